@@ -1,0 +1,256 @@
+"""Generate golden vectors by running the REFERENCE implementation.
+
+Run in the build container only (needs /root/reference):
+
+    PYTHONDONTWRITEBYTECODE=1 python tools/gen_golden.py
+
+It imports ``/root/reference/eks`` (with an empty ``seaborn`` stand-in module
+in ``sys.modules``: seaborn is imported by eks/newton_eks.py:8 but only used
+for a plot at :59, and is not installed here), runs the reference functions on
+seeded inputs and on the reference's own example data, and writes the inputs,
+every intermediate and the outputs as ``.npz`` fixtures to ``tests/golden/``.
+No reference source is copied; only numbers are written.  The fixtures are what
+travels to the GPU box; the reference does not.
+"""
+from __future__ import annotations
+
+import glob
+import os
+import sys
+import types
+
+import numpy as np
+import pandas as pd
+
+REF = "/root/reference"
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+OUT = os.path.join(REPO, "tests", "golden")
+
+sys.path.insert(0, REPO)
+from eks_amd import synthetic  # noqa: E402
+
+
+def _import_reference():
+    sys.dont_write_bytecode = True
+    sys.modules.setdefault("seaborn", types.ModuleType("seaborn"))
+    sys.path.insert(0, REF)
+    import eks.ensemble_kalman as ek  # noqa: F401
+    import eks.multiview_pca_smoother as mv  # noqa: F401
+    import eks.pupil_smoother as ps  # noqa: F401
+    import eks.utils as ut  # noqa: F401
+    return ek, mv, ps, ut
+
+
+def _save(name, **arrays):
+    os.makedirs(OUT, exist_ok=True)
+    path = os.path.join(OUT, name + ".npz")
+    np.savez_compressed(path, **arrays)
+    print(f"wrote {path} ({os.path.getsize(path) / 1024:.1f} KiB)")
+
+
+def _spd(rng, r, scale):
+    M = rng.normal(size=(r, r))
+    return scale * (M @ M.T / r + 0.5 * np.eye(r))
+
+
+# -------------------------------------------------------------------------
+def gen_core(ek):
+    """filtering_pass / smooth_backward / kalman_dot on random systems."""
+    cases = []
+    for (r, n) in [(2, 2), (3, 4), (3, 6), (3, 8), (2, 5), (4, 8)]:
+        for T in (1, 2, 3, 257):
+            cases.append((r, n, T, "rand"))
+    cases += [(2, 2, 1000, "rand"), (3, 8, 1000, "rand"), (2, 2, 300, "zero_var"),
+              (3, 4, 300, "zero_var"), (3, 8, 300, "diagA"), (2, 2, 2000, "heavy")]
+    for i, (r, n, T, kind) in enumerate(cases):
+        rng = np.random.default_rng(1000 + i)
+        A = np.eye(r) + 0.05 * rng.normal(size=(r, r))
+        if kind == "diagA":
+            A = np.diag(rng.uniform(0.95, 0.9999, size=r))
+        Q = _spd(rng, r, 0.5)
+        if kind == "heavy":
+            A = np.eye(r)
+            Q = _spd(rng, r, 1e-4)
+        S0 = _spd(rng, r, 20.0)
+        m0 = rng.normal(size=r)
+        C = rng.normal(size=(n, r)) * 2.0
+        x = np.cumsum(rng.normal(size=(T, r)), axis=0)
+        y = x @ C.T + rng.normal(size=(T, n))
+        ev = rng.uniform(0.05, 4.0, size=(T, n))
+        if kind == "zero_var":
+            # exact-agreement frames: one member-variance entry at zero in 20% of
+            # frames (several zeros at once can make R + C P C^T singular, where
+            # the reference's own answer is round-off noise)
+            rows = np.where(rng.random(size=T) < 0.2)[0]
+            ev[rows, rng.integers(0, n, size=len(rows))] = 0.0
+        R_in = np.eye(n)
+        R = R_in.copy()
+        mf, Vf, S = ek.filtering_pass(y, m0, S0, C, R, A, Q, ev)
+        if T >= 2:
+            ms, Vs, CV = ek.smooth_backward(y, mf, Vf, S, A, Q, C)
+        else:  # the reference's backward loop is empty for T == 1
+            ms, Vs, CV = mf.copy(), Vf.copy(), np.zeros((0, r, r))
+        vec = rng.normal(size=n)
+        mat = rng.normal(size=(n, r))
+        kd_vec = ek.kalman_dot(vec, S0, C, np.diag(ev[0]))
+        kd_mat = ek.kalman_dot(mat, S0, C, np.diag(ev[0]))
+        _save(f"core_{kind}_r{r}_n{n}_T{T}", y=y, m0=m0, S0=S0, C=C, R_in=R_in, A=A, Q=Q,
+              ev=ev, mf=mf, Vf=Vf, S=S, ms=ms, Vs=Vs, CV=CV, R_out=R,
+              kd_vec_in=vec, kd_mat_in=mat, kd_vec=kd_vec, kd_mat=kd_mat)
+
+
+def gen_ensemble(ek):
+    """ensemble() on member stacks, both modes, odd/even E, with NaNs."""
+    for E in (1, 2, 3, 4, 5, 8):
+        for mode in ("median", "mean"):
+            rng = np.random.default_rng(50 + E)
+            T, n = 64, 3
+            stack = rng.normal(100.0, 20.0, size=(E, T, n))
+            if E == 5:
+                stack[2, 7, 1] = np.nan
+            keys = [f"kp{j}" for j in range(n)]
+            dfs = [pd.DataFrame(stack[e], columns=keys) for e in range(E)]
+            preds, var, stacks, _, _, _ = ek.ensemble(dfs, keys, mode=mode)
+            _save(f"ensemble_E{E}_{mode}", stack=stack, preds=preds, vars=var, stacks=stacks)
+
+
+def gen_singleview(ek):
+    """Single-view definition computed with the reference's
+    ensemble/filtering_pass/smooth_backward."""
+    for name, (E, T, seed, s, q) in {"c1": (3, 1000, 0, 0.01, 25.0),
+                                      "c2small": (5, 3000, 2, 0.01, 25.0),
+                                      "q100": (4, 500, 7, 0.5, 100.0)}.items():
+        rng = np.random.default_rng(seed)
+        obs = synthetic.singleview_obs(rng, E, T, K=1)[:, :, 0, :].astype(np.float64)
+        keys = ["kp_x", "kp_y"]
+        dfs = [pd.DataFrame(obs[e], columns=keys) for e in range(E)]
+        preds, ev, _, _, _, _ = ek.ensemble(dfs, keys)
+        max_vars = np.max(ev, 1)
+        good = np.where(max_vars <= np.percentile(max_vars, q))[0]
+        means = preds[good].mean(axis=0)
+        y = preds - means
+        gy = y[good]
+        m0 = np.zeros(2)
+        S0 = np.diag(np.var(gy, axis=0))
+        A = np.eye(2)
+        C = np.eye(2)
+        Q = s * np.cov((gy[1:] - gy[:-1]).T)
+        R = np.eye(2)
+        mf, Vf, S = ek.filtering_pass(y, m0, S0, C, R, A, Q, ev)
+        ms, Vs, _ = ek.smooth_backward(y, mf, Vf, S, A, Q, C)
+        out = (C @ ms.T).T + means
+        _save(f"singleview_{name}", obs=obs, s=s, q=q, preds=preds, ev=ev, means=means,
+              m0=m0, S0=S0, A=A, C=C, Q=Q, mf=mf, Vf=Vf, S=S, ms=ms, Vs=Vs, out=out)
+
+
+def _mouse_markers(ut):
+    files = sorted(glob.glob(os.path.join(REF, "data/mirror-mouse/*.csv")))
+    markers = []
+    for f in files:
+        df = pd.read_csv(f, header=[0, 1, 2], index_col=0)
+        kps = [c[1] for c in df.columns[::3]]
+        markers.append(ut.convert_lp_dlc(df, kps, model_name=df.columns[0][0]))
+    return markers
+
+
+def gen_multicam(mv, ut):
+    """mirror-mouse: reference pipeline (s=.01, q=25) for one paw, full T, plus
+    the committed golden eks.csv columns for that paw."""
+    markers = _mouse_markers(ut)
+    cams = ["top", "bot"]
+    golden = pd.read_csv(os.path.join(REF, "data/mirror-mouse/output/eks.csv"),
+                         header=[0, 1, 2], index_col=0)
+    for paw in ("paw2LF", "paw4RH"):
+        by_cam = [[] for _ in cams]
+        stacks = []
+        for c, cam in enumerate(cams):
+            cols = [f"{paw}_{cam}_x", f"{paw}_{cam}_y"]
+            for m in markers:
+                by_cam[c].append(m[cols])
+            stacks.append(np.stack([m[cols].to_numpy() for m in markers]))  # (E,T,2)
+        dfs = mv.ensemble_kalman_smoother_multi_cam(by_cam, paw, 0.01, 25, cams)
+        out = np.concatenate(
+            [dfs[f"{cam}_df"].loc[:, ("ensemble-kalman_tracker", paw, c)].to_numpy()[:, None]
+             for cam in cams for c in ("x", "y")], axis=1)
+        gold = np.concatenate(
+            [golden.loc[:, ("ensemble-kalman_tracker", f"{paw}_{cam}", c)].to_numpy()[:, None]
+             for cam in cams for c in ("x", "y")], axis=1)
+        print(f"  {paw}: reference re-run vs committed golden max|d| = {np.abs(out - gold).max():.2e}")
+        _save(f"multicam_mouse_{paw}", stacks=np.stack(stacks), s=0.01, q=25.0, out=out, golden=gold)
+
+
+def gen_fish(ut, mv):
+    """mirror-fish clips (3 cams, T=51, s=.01, q=50) vs the committed
+    test_script.py outputs in data/misc/mirror-fish_ensemble-predictions/eks."""
+    base = os.path.join(REF, "data/misc/mirror-fish_ensemble-predictions")
+    cams = ["main", "top", "right"]
+    tracker = "heatmap_mhcrnn_tracker"
+    clips = [("20210126_Sean", "img001058.csv"), ("20210202_Quin", None)]
+    for session, frame in clips:
+        if frame is None:
+            frame = sorted(os.listdir(os.path.join(base, "network_0", session)))[0]
+        markers = []
+        for k in range(5):
+            df = pd.read_csv(os.path.join(base, f"network_{k}", session, frame), header=[0, 1, 2],
+                             index_col=0)
+            kps = [c[1] for c in df.columns[::3]]
+            markers.append(ut.convert_lp_dlc(df, kps, model_name=tracker))
+        golden = pd.read_csv(os.path.join(base, "eks", session, frame), header=[0, 1, 2], index_col=0)
+        for kp in ("head", "mid"):
+            stacks, by_cam = [], [[] for _ in cams]
+            for c, cam in enumerate(cams):
+                cols = [k for k in markers[0].keys() if cam in k and "likelihood" not in k and kp in k]
+                for m in markers:
+                    by_cam[c].append(m[cols])
+                stacks.append(np.stack([m[cols].to_numpy() for m in markers]))
+            dfs = mv.ensemble_kalman_smoother_multi_cam(by_cam, kp, 0.01, 50, cams)
+            out = np.concatenate(
+                [dfs[f"{cam}_df"].loc[:, ("ensemble-kalman_tracker", kp, c)].to_numpy()[:, None]
+                 for cam in cams for c in ("x", "y")], axis=1)
+            gold = np.concatenate(
+                [golden.loc[:, (tracker, f"{kp}_{cam}", c)].to_numpy()[:, None]
+                 for cam in cams for c in ("x", "y")], axis=1)
+            print(f"  fish {session}/{frame}/{kp}: re-run vs golden max|d| = {np.abs(out - gold).max():.2e}")
+            _save(f"multicam_fish_{session}_{kp}", stacks=np.stack(stacks), s=0.01, q=50.0,
+                  out=out, golden=gold)
+
+
+def gen_pupil(ps, ut):
+    """ibl-pupil with A = diag(.99,.99,.99) (scripts/readme.txt:7) vs the committed
+    golden kalman_smoothed_*.csv."""
+    files = sorted(glob.glob(os.path.join(REF, "data/ibl-pupil/*.csv")))
+    markers = []
+    for f in files:
+        df = pd.read_csv(f, header=[0, 1, 2], index_col=0)
+        kps = [c[1] for c in df.columns[::3]]
+        markers.append(ut.convert_lp_dlc(df, kps, model_name=df.columns[0][0]))
+    A = np.diag([0.99, 0.99, 0.99])
+    res = ps.ensemble_kalman_smoother_pupil(markers, kps, "ensemble-kalman_tracker", A)
+    keys = ['pupil_top_r_x', 'pupil_top_r_y', 'pupil_bottom_r_x', 'pupil_bottom_r_y',
+            'pupil_right_r_x', 'pupil_right_r_y', 'pupil_left_r_x', 'pupil_left_r_y']
+    stack = np.stack([m[keys].to_numpy() for m in markers])
+    mk = res["markers_df"].to_numpy()
+    lat = res["latents_df"].to_numpy()
+    g_mk = pd.read_csv(os.path.join(REF, "data/misc/pupil-test/kalman_smoothed_pupil_traces.csv"),
+                       header=[0, 1, 2], index_col=0).to_numpy()
+    g_lat = pd.read_csv(os.path.join(REF, "data/misc/pupil-test/kalman_smoothed_latents.csv"),
+                        header=[0, 1], index_col=0).to_numpy()
+    print(f"  pupil: markers re-run vs golden {np.nanmax(np.abs(mk - g_mk)):.2e}, "
+          f"latents {np.abs(lat - g_lat).max():.2e}")
+    _save("pupil_ibl", stack=stack, A=A, markers=mk, latents=lat, golden_markers=g_mk,
+          golden_latents=g_lat, keypoint_names=np.array(kps))
+
+
+def main():
+    ek, mv, ps, ut = _import_reference()
+    gen_core(ek)
+    gen_ensemble(ek)
+    gen_singleview(ek)
+    gen_multicam(mv, ut)
+    gen_fish(ut, mv)
+    gen_pupil(ps, ut)
+
+
+if __name__ == "__main__":
+    main()
