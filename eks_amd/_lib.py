@@ -1,0 +1,95 @@
+"""ctypes binding of libeks_hip.so (the C ABI in include/eks_hip.h).
+
+The HIP library is the product: there is no CPU fallback.  Loading fails with
+an ImportError-style RuntimeError naming the missing file, and every compute
+call requires a visible GPU (``torch.cuda.is_available()``).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libeks_hip.so")
+HEADER = os.path.join(os.path.dirname(HERE), "include", "eks_hip.h")
+
+EKS_OK, EKS_ERR_ARG, EKS_ERR_UNSUPPORTED, EKS_SINGULAR, EKS_ERR_HIP = 0, 1, 2, 3, 4
+EKS_F32, EKS_F64 = 0, 1
+EKS_MEDIAN, EKS_MEAN = 0, 1
+
+_p = C.c_void_p
+_i64 = C.c_int64
+_i32 = C.c_int
+_sz = C.c_size_t
+
+# argument types of every exported entry point (order as in the header)
+SIGNATURES = {
+    "eks_last_error": (C.c_char_p, []),
+    "eks_version": (_i32, []),
+    "eks_max_latent": (_i32, []),
+    "eks_max_obs": (_i32, []),
+    "eks_max_members": (_i32, []),
+    "eks_ensemble": (_i32, [_p, _i32, _i64, _i64, _i32, _i32, _i64, _i64, _i64, _i64, _i32,
+                            _p, _p, _p]),
+    "eks_forward": (_i32, [_i64, _i64, _i32, _i32, _p, _p, _p, _p, _p, _p, _p, _p, _i32,
+                           _p, _p, _p, _p, _p, _p]),
+    "eks_backward": (_i32, [_i64, _i64, _i32, _p, _p, _p, _p, _i32, _p, _p, _p, _p, _p]),
+    "eks_kalman_dot": (_i32, [_i32, _i32, _i32, _p, _p, _p, _p, _p, _p, _p]),
+    "eks_param_len": (_i64, [_i32, _i32]),
+    "eks_smooth_workspace_bytes": (_sz, [_i64, _i64, _i32, _i32, _i32]),
+    "eks_smooth": (_i32, [_p, _i32, _i64, _i64, _i32, _i32, _i32, _i64, _i64, _i64, _i64, _i32,
+                          _p, _p, _i64, _i64, _i64, _p, _p, _p, _sz, _i32, _p, _p]),
+}
+
+_lib = None
+
+
+class EksError(RuntimeError):
+    """A libeks_hip call returned an error code."""
+
+
+def header_symbols() -> list[str]:
+    """Function names declared in include/eks_hip.h."""
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(eks_[a-z_0-9]+)\s*\(", src)))
+
+
+def load():
+    """Load (once) and return the ctypes library handle."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f"{LIB_PATH} is missing: build the HIP extension first "
+            f"(python -m eks_amd.build, or __graft_entry__.build()). "
+            f"eks_amd has no CPU fallback.")
+    lib = C.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(code: int, what: str) -> None:
+    if code != EKS_OK:
+        msg = load().eks_last_error().decode(errors="replace")
+        raise EksError(f"{what} failed (code {code}): {msg}")
+
+
+def require_gpu():
+    import torch
+    if not torch.cuda.is_available():
+        raise RuntimeError("eks_amd needs an AMD GPU (MI355X / gfx950): no HIP device is "
+                           "visible, and there is no CPU fallback")
+    return torch
+
+
+def stream_ptr(stream=None) -> int:
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return int(s.cuda_stream)

@@ -1,0 +1,121 @@
+"""Batched, device-resident API of the fused smoother (the throughput path).
+
+    out = smooth(obs, params, n=..., r=...)
+
+``obs`` is a CUDA tensor viewed as (B, T, E, n) -- B trajectories (video x
+keypoint), T frames, E ensemble members, n observed coordinates -- float32 or
+float64, ANY strides (the kernel reads obs[b*sb + t*st + e*se + j*sj]).
+For coalesced loads give it a layout whose trajectory axis is innermost, e.g.
+a contiguous (T, E, n, B) buffer viewed with ``.permute(3, 0, 1, 2)``:
+that is what ``bench.py`` and ``make_time_major`` use.
+
+``params`` is the (B, P) float64 tensor from ``pack_params``.  Nothing is
+copied to the host; everything is stream-ordered on the current stream.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _lib
+
+_WS = {}
+
+
+def param_len(n: int, r: int) -> int:
+    return r + 3 * r * r + n * r + n
+
+
+def pack_params(m0, S0, A, Q, C, offset, device="cuda"):
+    """Pack per-trajectory models into the (B, P) layout of eks_param_len:
+    [m0 (r) | S0 (r*r) | A (r*r) | Q (r*r) | C (n*r) | offset (n)].
+    Inputs are arrays/tensors with a leading B axis (or none, = shared)."""
+    import torch
+
+    def t(x):
+        x = torch.as_tensor(np.asarray(x) if not isinstance(x, torch.Tensor) else x,
+                            dtype=torch.float64)
+        return x
+
+    m0, S0, A, Q, C, offset = map(t, (m0, S0, A, Q, C, offset))
+    r = m0.shape[-1]
+    n = offset.shape[-1]
+    parts = [m0, S0, A, Q, C, offset]
+    B = max(p.shape[0] if p.dim() == d else 1 for p, d in zip(parts, (2, 3, 3, 3, 3, 2)))
+    flat = []
+    for p, d in zip(parts, (2, 3, 3, 3, 3, 2)):
+        if p.dim() == d - 1:
+            p = p.unsqueeze(0).expand(B, *p.shape)
+        flat.append(p.reshape(B, -1))
+    out = torch.cat(flat, dim=1).contiguous().to(device)
+    assert out.shape[1] == param_len(n, r)
+    return out
+
+
+def workspace(nbytes: int, device=None):
+    import torch
+    dev = torch.device("cuda") if device is None else torch.device(device)
+    key = (dev.index if dev.index is not None else torch.cuda.current_device())
+    buf = _WS.get(key)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=dev)
+        _WS[key] = buf
+    return buf
+
+
+def smooth(obs, params, *, n: int, r: int, mode: str = "median", out=None, want_ms=False,
+           want_nll=False, status=None, algo: int = 0, stream=None):
+    """Fused ensemble -> forward -> backward -> projection for B trajectories.
+
+    Returns dict(out=(B,T,n) view, ms=(B,T,r) or None, nll=(B,) or None,
+    status=(B,) int32).  ``out`` (if given) must be a (B, T, n) float64 CUDA
+    tensor/view; by default a time-major buffer is allocated so that the
+    kernel's stores are coalesced.
+    """
+    torch = _lib.require_gpu()
+    if obs.dim() != 4:
+        raise ValueError("obs must be viewed as (B, T, E, n)")
+    B, T, E, nn = obs.shape
+    if nn != n:
+        raise ValueError(f"obs has {nn} coordinates, expected n={n}")
+    if obs.dtype == torch.float32:
+        dt = _lib.EKS_F32
+    elif obs.dtype == torch.float64:
+        dt = _lib.EKS_F64
+    else:
+        raise TypeError("obs must be float32 or float64")
+    if mode not in ("median", "mean"):
+        raise ValueError(f"{mode} averaging not supported")
+    if params.shape != (B, param_len(n, r)) or params.dtype != torch.float64 \
+            or not params.is_contiguous():
+        raise ValueError(f"params must be a contiguous ({B}, {param_len(n, r)}) float64 tensor")
+    dev = obs.device
+    if out is None:
+        out = torch.empty((T, B, n), dtype=torch.float64, device=dev).permute(1, 0, 2)
+    ms = torch.empty((B, T, r), dtype=torch.float64, device=dev) if want_ms else None
+    nll = torch.empty((B,), dtype=torch.float64, device=dev) if want_nll else None
+    if status is None:
+        status = torch.empty((B,), dtype=torch.int32, device=dev)
+    lib = _lib.load()
+    nbytes = lib.eks_smooth_workspace_bytes(B, T, n, r, algo)
+    ws = workspace(nbytes, dev)
+    sb, st, se, sj = obs.stride()
+    ob, ot, oj = out.stride()
+    _lib.check(lib.eks_smooth(
+        obs.data_ptr(), dt, B, T, E, n, r, sb, st, se, sj,
+        _lib.EKS_MEDIAN if mode == "median" else _lib.EKS_MEAN, params.data_ptr(),
+        out.data_ptr(), ob, ot, oj, ms.data_ptr() if ms is not None else None,
+        nll.data_ptr() if nll is not None else None, ws.data_ptr(), ws.numel(), algo,
+        status.data_ptr(), _lib.stream_ptr(stream)), "eks_smooth")
+    return dict(out=out, ms=ms, nll=nll, status=status)
+
+
+def make_time_major(stack_np, device="cuda", dtype=None):
+    """(B, E, T, n) numpy array -> CUDA tensor stored (T, E, n, B), returned as
+    the (B, T, E, n) view the kernels read with coalesced per-lane loads."""
+    import torch
+    a = np.asarray(stack_np)
+    if dtype is not None:
+        a = a.astype(dtype)
+    tm = np.ascontiguousarray(np.transpose(a, (2, 1, 3, 0)))  # (T, E, n, B)
+    d = torch.from_numpy(tm).to(device)
+    return d.permute(3, 0, 1, 2)

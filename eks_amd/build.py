@@ -1,0 +1,94 @@
+"""Build libeks_hip.so for gfx950 in-tree (eks_amd/lib/).
+
+    python -m eks_amd.build          # incremental
+    python -m eks_amd.build --force  # rebuild everything
+
+Each ``csrc/*.hip`` translation unit is compiled by ``hipcc
+--offload-arch=gfx950`` (cross-compiles without a GPU) into an object file,
+then all objects are linked into one shared library with a plain C ABI
+(include/eks_hip.h).  The library is what the Python package binds with
+ctypes; it is built in the tree so that it travels with the repository
+snapshot to the GPU box.
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import glob
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+LIBDIR = os.path.join(HERE, "lib")
+OBJDIR = os.path.join(LIBDIR, "obj")
+LIBNAME = "libeks_hip.so"
+ARCH = os.environ.get("EKS_OFFLOAD_ARCH", "gfx950")
+HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall",
+          "-Wno-unused-function", "-Wno-unused-variable", "-Wno-unused-but-set-variable"]
+
+
+def lib_path() -> str:
+    return os.path.join(LIBDIR, LIBNAME)
+
+
+def _deps() -> list[str]:
+    return sorted(glob.glob(os.path.join(CSRC, "*.hpp")) +
+                  glob.glob(os.path.join(REPO, "include", "*.h")))
+
+
+def _stale(target: str, sources: list[str]) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(s) > t for s in sources)
+
+
+def _compile(src: str, obj: str) -> None:
+    cmd = [HIPCC, *CFLAGS, "-c", src, "-o", obj]
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError(f"hipcc failed on {src}:\n{res.stderr[-6000:]}")
+
+
+def build(force: bool = False, jobs: int | None = None, verbose: bool = True) -> str:
+    os.makedirs(OBJDIR, exist_ok=True)
+    srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+    deps = _deps()
+    todo = []
+    objs = []
+    for s in srcs:
+        o = os.path.join(OBJDIR, os.path.basename(s)[:-4] + ".o")
+        objs.append(o)
+        if force or _stale(o, [s, *deps]):
+            todo.append((s, o))
+    if todo:
+        jobs = jobs or min(len(todo), max(1, (os.cpu_count() or 2) // 2), 8)
+        if verbose:
+            print(f"[eks_amd.build] compiling {len(todo)} unit(s) for {ARCH} with {jobs} job(s)")
+        with cf.ThreadPoolExecutor(jobs) as ex:
+            for fut in [ex.submit(_compile, s, o) for s, o in todo]:
+                fut.result()
+    lib = lib_path()
+    if todo or _stale(lib, objs):
+        cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", lib + ".tmp"]
+        res = subprocess.run(cmd, capture_output=True, text=True)
+        if res.returncode != 0:
+            raise RuntimeError(f"link failed:\n{res.stderr[-4000:]}")
+        os.replace(lib + ".tmp", lib)
+        if verbose:
+            print(f"[eks_amd.build] linked {lib}")
+    return lib
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-j", "--jobs", type=int, default=None)
+    a = ap.parse_args()
+    build(force=a.force, jobs=a.jobs)
+    sys.exit(0)

@@ -1,0 +1,435 @@
+// HIP kernels and C ABI of libeks_hip.so (see include/eks_hip.h).
+//
+// Target: gfx950 (MI355X, CDNA4), wave64.  Everything on the recursion path
+// is float64 in VGPRs; per-step matrices are at most 8x8, so there is no
+// MFMA here (DESIGN.md explains the roofline: the fused path is bound by HBM
+// bandwidth and FP64 issue, not by matrix throughput).
+//
+// Kernels
+//   k_ensemble        eks/ensemble_kalman.py:4-57     one thread per (b, t, j)
+//   k_forward_dense   eks/ensemble_kalman.py:59-117   one lane per trajectory,
+//                     LU solve of the n x n innovation covariance exactly as
+//                     the reference's kalman_dot (drop-in API, full R)
+//   k_backward        eks/ensemble_kalman.py:120-164  one lane per trajectory
+//   k_kalman_dot      eks/ensemble_kalman.py:110-117
+//   k_smooth_seq      fused hot path, one lane per trajectory: ensemble ->
+//                     forward (sequential scalar updates, R diagonal) ->
+//                     RTS backward -> projection; time-major workspace
+// The time-parallel chunked-scan kernels live in eks_chunked.hip.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <algorithm>
+
+#include "../../include/eks_hip.h"
+#include "ensemble.hpp"
+#include "eks_common.hpp"
+#include "small_linalg.hpp"
+
+namespace eks {
+
+// ------------------------------------------------------------------------
+// error reporting
+// ------------------------------------------------------------------------
+static thread_local std::string g_err;
+
+int set_err(int code, const char *fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+int check_launch(const char *what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return set_err(EKS_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
+  return EKS_OK;
+}
+
+// ------------------------------------------------------------------------
+// A1: ensemble reduction, one thread per (b, t, j)
+// ------------------------------------------------------------------------
+template <int E, typename T>
+__global__ __launch_bounds__(256) void k_ensemble(const T *__restrict__ obs, long long B,
+                                                  long long TT, int Ert, int n, long long sb,
+                                                  long long st, long long se, long long sj,
+                                                  int median, double *__restrict__ preds,
+                                                  double *__restrict__ vars) {
+  const long long total = B * TT * n;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long j = i % n;
+    const long long bt = i / n;
+    const long long t = bt % TT;
+    const long long b = bt / TT;
+    const T *p = obs + b * sb + t * st + j * sj;
+    double avg, var;
+    if constexpr (E > 0) {
+      T raw[E];
+#pragma unroll
+      for (int e = 0; e < E; ++e) raw[e] = p[e * se];
+      ensemble_reduce<E, T>(raw, median != 0, avg, var);
+    } else {
+      ensemble_reduce_rt<T>(p, se, Ert, median != 0, avg, var);
+    }
+    preds[i] = avg;
+    vars[i] = var;
+  }
+}
+
+// ------------------------------------------------------------------------
+// A2/A3: drop-in forward filter with the dense n x n solve of kalman_dot
+// ------------------------------------------------------------------------
+template <int R, int N>
+__global__ __launch_bounds__(64) void k_forward_dense(
+    long long B, long long TT, const double *__restrict__ y, const double *__restrict__ ev,
+    const double *__restrict__ m0g, const double *__restrict__ S0g, const double *__restrict__ Ag,
+    const double *__restrict__ Qg, const double *__restrict__ Cg, const double *__restrict__ Rg,
+    int shared, double *__restrict__ mf, double *__restrict__ Vf, double *__restrict__ S,
+    double *__restrict__ nll, int32_t *__restrict__ status) {
+  const long long b = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const long long pb = shared ? 0 : b;
+  double A[R][R], Q[R][R], C[N][R], Roff[N][N], m[R], P[R][R];
+  load_mat<R, R>(Ag + pb * R * R, A);
+  load_mat<R, R>(Qg + pb * R * R, Q);
+  load_mat<N, R>(Cg + pb * N * R, C);
+  if (Rg) {
+    load_mat<N, N>(Rg + pb * N * N, Roff);
+  } else {
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+#pragma unroll
+      for (int j = 0; j < N; ++j) Roff[i][j] = 0.0;
+  }
+  load_vec<R>(m0g + pb * R, m);
+  load_mat<R, R>(S0g + pb * R * R, P);
+
+  const double *yb = y + b * TT * N;
+  const double *eb = ev + b * TT * N;
+  double *mfb = mf ? mf + b * TT * R : nullptr;
+  double *Vfb = Vf ? Vf + b * TT * R * R : nullptr;
+  double *Sb = S ? S + b * TT * R * R : nullptr;
+  bool ok = true;
+  double quad = 0.0, det_m = 1.0;
+  int det_e = 0;
+  double mprev[R], Vprev[R][R];
+  for (long long t = 0; t < TT; ++t) {
+    if (t > 0) {
+      // S[t-1] = A Vf[t-1] A^T + Q  (:101); prior mean A mf[t-1]  (:102)
+      double VAt[R][R];
+      matmul_nt<R, R, R>(Vprev, A, VAt);
+      matmul<R, R, R>(A, VAt, P);
+#pragma unroll
+      for (int i = 0; i < R; ++i)
+#pragma unroll
+        for (int j = 0; j < R; ++j) P[i][j] += Q[i][j];
+      matvec<R, R>(A, mprev, m);
+      if (Sb) store_mat<R, R>(Sb + (t - 1) * R * R, P);
+    } else if (Sb) {
+      store_mat<R, R>(Sb, P);  // S[0] = S0 (:96); overwritten at t = 1
+    }
+    // innovation covariance R_t + C (P C^T)   (:112)
+    double PCt[R][N], sig[N][N];
+    matmul_nt<R, R, N>(P, C, PCt);
+    matmul<N, R, N>(C, PCt, sig);
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+#pragma unroll
+      for (int j = 0; j < N; ++j) sig[i][j] += (i == j) ? eb[t * N + i] : Roff[i][j];
+    // right-hand sides [ y - C m | C P ]  (:94-95, :102-105)
+    double rhs[N][1 + R], e0[N];
+    double Cm[N];
+    matvec<N, R>(C, m, Cm);
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      e0[i] = yb[t * N + i] - Cm[i];
+      rhs[i][0] = e0[i];
+#pragma unroll
+      for (int j = 0; j < R; ++j) {
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < R; ++k) s = fma(C[i][k], P[k][j], s);
+        rhs[i][1 + j] = s;
+      }
+    }
+    ok = gauss_solve<N, 1 + R>(sig, rhs, det_m, det_e) && ok;
+#pragma unroll
+    for (int i = 0; i < N; ++i) quad = fma(e0[i], rhs[i][0], quad);
+    // mf = m + P (C^T x0);  Vf = P - P (C^T X)
+    double ctx[R][1 + R];
+#pragma unroll
+    for (int k = 0; k < R; ++k)
+#pragma unroll
+      for (int c = 0; c < 1 + R; ++c) {
+        double s = 0.0;
+#pragma unroll
+        for (int i = 0; i < N; ++i) s = fma(C[i][k], rhs[i][c], s);
+        ctx[k][c] = s;
+      }
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      double s = 0.0;
+#pragma unroll
+      for (int k = 0; k < R; ++k) s = fma(P[i][k], ctx[k][0], s);
+      mprev[i] = m[i] + s;
+#pragma unroll
+      for (int j = 0; j < R; ++j) {
+        double u = 0.0;
+#pragma unroll
+        for (int k = 0; k < R; ++k) u = fma(P[i][k], ctx[k][1 + j], u);
+        Vprev[i][j] = P[i][j] - u;
+      }
+    }
+    if (mfb) store_vec<R>(mfb + t * R, mprev);
+    if (Vfb) store_mat<R, R>(Vfb + t * R * R, Vprev);
+  }
+  if (Sb && TT >= 2) {
+    double z[R][R] = {};
+    store_mat<R, R>(Sb + (TT - 1) * R * R, z);  // never written by the reference
+  }
+  if (nll) nll[b] = 0.5 * ((double)TT * N * kLog2Pi + log(det_m) + det_e * kLn2 + quad);
+  if (status) status[b] = ok ? 0 : EKS_SINGULAR;
+}
+
+// ------------------------------------------------------------------------
+// A4: drop-in RTS backward pass
+// ------------------------------------------------------------------------
+template <int R>
+__global__ __launch_bounds__(64) void k_backward(long long B, long long TT,
+                                                 const double *__restrict__ mf,
+                                                 const double *__restrict__ Vf,
+                                                 const double *__restrict__ S,
+                                                 const double *__restrict__ Ag, int shared,
+                                                 double *__restrict__ ms, double *__restrict__ Vs,
+                                                 double *__restrict__ CV,
+                                                 int32_t *__restrict__ status) {
+  const long long b = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  double A[R][R];
+  load_mat<R, R>(Ag + (shared ? 0 : b) * R * R, A);
+  const double *mfb = mf + b * TT * R;
+  const double *Vfb = Vf + b * TT * R * R;
+  const double *Sb = S + b * TT * R * R;
+  double msn[R], Vsn[R][R];
+  load_vec<R>(mfb + (TT - 1) * R, msn);
+  load_mat<R, R>(Vfb + (TT - 1) * R * R, Vsn);
+  if (ms) store_vec<R>(ms + b * TT * R + (TT - 1) * R, msn);
+  if (Vs) store_mat<R, R>(Vs + b * TT * R * R + (TT - 1) * R * R, Vsn);
+  bool ok = true;
+  for (long long t = TT - 2; t >= 0; --t) {
+    double mft[R], Vft[R][R], St[R][R], X[R][R];
+    load_vec<R>(mfb + t * R, mft);
+    load_mat<R, R>(Vfb + t * R * R, Vft);
+    load_mat<R, R>(Sb + t * R * R, St);
+    double Sc[R][R];
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+#pragma unroll
+      for (int j = 0; j < R; ++j) Sc[i][j] = St[i][j];
+    matmul<R, R, R>(A, Vft, X);            // rhs = A Vf[t]
+    ok = gauss_solve<R, R>(Sc, X) && ok;   // X = S^-1 A Vf ; J = X^T  (:158)
+    // ms = mf + J (ms[t+1] - A mf)  (:161)
+    double Amf[R], d[R];
+    matvec<R, R>(A, mft, Amf);
+#pragma unroll
+    for (int i = 0; i < R; ++i) d[i] = msn[i] - Amf[i];
+    double msc[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      double s = 0.0;
+#pragma unroll
+      for (int k = 0; k < R; ++k) s = fma(X[k][i], d[k], s);
+      msc[i] = mft[i] + s;
+    }
+    if (Vs || CV) {
+      // W = (Vs[t+1] - S) J^T ; Vs[t] = Vf + J W  (:160) ; CV[t] = Vs[t+1] J^T (:162)
+      double D[R][R], W[R][R], CVt[R][R], Vsc[R][R];
+#pragma unroll
+      for (int i = 0; i < R; ++i)
+#pragma unroll
+        for (int j = 0; j < R; ++j) D[i][j] = Vsn[i][j] - St[i][j];
+      // J^T = X, so (D J^T) = D X
+      matmul<R, R, R>(D, X, W);
+      matmul<R, R, R>(Vsn, X, CVt);
+#pragma unroll
+      for (int i = 0; i < R; ++i)
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+          double s = 0.0;
+#pragma unroll
+          for (int k = 0; k < R; ++k) s = fma(X[k][i], W[k][j], s);
+          Vsc[i][j] = Vft[i][j] + s;
+        }
+      if (CV) store_mat<R, R>(CV + b * (TT - 1) * R * R + t * R * R, CVt);
+      if (Vs) store_mat<R, R>(Vs + b * TT * R * R + t * R * R, Vsc);
+#pragma unroll
+      for (int i = 0; i < R; ++i)
+#pragma unroll
+        for (int j = 0; j < R; ++j) Vsn[i][j] = Vsc[i][j];
+    }
+    if (ms) store_vec<R>(ms + b * TT * R + t * R, msc);
+#pragma unroll
+    for (int i = 0; i < R; ++i) msn[i] = msc[i];
+  }
+  if (status) status[b] = ok ? 0 : EKS_SINGULAR;
+}
+
+// ------------------------------------------------------------------------
+// A3: kalman_dot, one problem, one thread (the reference calls it per step)
+// ------------------------------------------------------------------------
+template <int R, int N>
+__global__ void k_kalman_dot(int k, const double *x, const double *Vg, const double *Cg,
+                             const double *Rg, double *out, int32_t *status) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  double V[R][R], C[N][R], Rm[N][N];
+  load_mat<R, R>(Vg, V);
+  load_mat<N, R>(Cg, C);
+  load_mat<N, N>(Rg, Rm);
+  double VCt[R][N], sig[N][N];
+  matmul_nt<R, R, N>(V, C, VCt);  // V C^T
+  matmul<N, R, N>(C, VCt, sig);   // C (V C^T)
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+#pragma unroll
+    for (int j = 0; j < N; ++j) sig[i][j] += Rm[i][j];
+  bool ok = true;
+  for (int c = 0; c < k; ++c) {
+    double a[N][N], rhs[N][1];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      rhs[i][0] = x[i * k + c];
+#pragma unroll
+      for (int j = 0; j < N; ++j) a[i][j] = sig[i][j];
+    }
+    ok = gauss_solve<N, 1>(a, rhs) && ok;
+    double ct[R];
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+      double s = 0.0;
+#pragma unroll
+      for (int i = 0; i < N; ++i) s = fma(C[i][q], rhs[i][0], s);
+      ct[q] = s;
+    }
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      double s = 0.0;
+#pragma unroll
+      for (int q = 0; q < R; ++q) s = fma(V[i][q], ct[q], s);
+      out[i * k + c] = s;
+    }
+  }
+  if (status) status[0] = ok ? 0 : EKS_SINGULAR;
+}
+
+}  // namespace eks
+
+// ==========================================================================
+// C ABI
+// ==========================================================================
+using namespace eks;
+
+extern "C" {
+
+const char *eks_last_error(void) { return g_err.c_str(); }
+int eks_version(void) { return 100; }
+int eks_max_latent(void) { return kMaxLatent; }
+int eks_max_obs(void) { return kMaxObs; }
+int eks_max_members(void) { return kMaxMembers; }
+int64_t eks_param_len(int n, int r) { return param_len(n, r); }
+
+int eks_ensemble(const void *obs, int obs_dtype, int64_t B, int64_t T, int E, int n, int64_t sb,
+                 int64_t st, int64_t se, int64_t sj, int mode, double *preds, double *vars,
+                 void *stream) {
+  g_err.clear();
+  if (!obs || !preds || !vars) return set_err(EKS_ERR_ARG, "eks_ensemble: NULL pointer");
+  if (B < 0 || T < 0 || n < 1 || E < 1) return set_err(EKS_ERR_ARG, "eks_ensemble: bad sizes");
+  if (E > kMaxMembers) return set_err(EKS_ERR_UNSUPPORTED, "eks_ensemble: E=%d > %d", E, kMaxMembers);
+  if (mode != EKS_MEDIAN && mode != EKS_MEAN)
+    return set_err(EKS_ERR_ARG, "%d averaging not supported", mode);
+  if (obs_dtype != EKS_F32 && obs_dtype != EKS_F64) return set_err(EKS_ERR_ARG, "bad dtype");
+  const long long total = (long long)B * T * n;
+  if (total == 0) return EKS_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const unsigned grid = (unsigned)std::min<long long>(grid_for(total, 256), 8192);
+  auto launch = [&](auto Ec, auto tag) -> int {
+    using Tp = decltype(tag);
+    constexpr int EE = decltype(Ec)::value;
+    hipLaunchKernelGGL((k_ensemble<EE, Tp>), dim3(grid), dim3(256), 0, s, (const Tp *)obs, B, T,
+                       E, n, sb, st, se, sj, mode == EKS_MEDIAN ? 1 : 0, preds, vars);
+    return check_launch("k_ensemble");
+  };
+  auto by_e = [&](auto tag) -> int {
+    switch (E) {
+      case 1: return launch(ic<1>{}, tag);
+      case 2: return launch(ic<2>{}, tag);
+      case 3: return launch(ic<3>{}, tag);
+      case 4: return launch(ic<4>{}, tag);
+      case 5: return launch(ic<5>{}, tag);
+      case 6: return launch(ic<6>{}, tag);
+      case 8: return launch(ic<8>{}, tag);
+      default: return launch(ic<0>{}, tag);
+    }
+  };
+  return obs_dtype == EKS_F32 ? by_e(float{}) : by_e(double{});
+}
+
+int eks_forward(int64_t B, int64_t T, int n, int r, const double *y, const double *ev,
+                const double *m0, const double *S0, const double *A, const double *Q,
+                const double *C, const double *R, int params_shared, double *mf, double *Vf,
+                double *S, double *nll, int32_t *status, void *stream) {
+  g_err.clear();
+  if (!y || !ev || !m0 || !S0 || !A || !Q || !C)
+    return set_err(EKS_ERR_ARG, "eks_forward: NULL input");
+  if (B < 0 || T < 1) return set_err(EKS_ERR_ARG, "eks_forward: need B >= 0, T >= 1");
+  if (B == 0) return EKS_OK;
+  hipStream_t s = (hipStream_t)stream;
+  return dispatch_r(r, [&](auto Rc) {
+    return dispatch_n(n, [&](auto Nc) {
+      constexpr int RR = decltype(Rc)::value, NN = decltype(Nc)::value;
+      hipLaunchKernelGGL((k_forward_dense<RR, NN>), dim3(grid_for(B, 64)), dim3(64), 0, s, B, T,
+                         y, ev, m0, S0, A, Q, C, R, params_shared, mf, Vf, S, nll, status);
+      return check_launch("k_forward_dense");
+    });
+  });
+}
+
+int eks_backward(int64_t B, int64_t T, int r, const double *mf, const double *Vf, const double *S,
+                 const double *A, int params_shared, double *ms, double *Vs, double *CV,
+                 int32_t *status, void *stream) {
+  g_err.clear();
+  if (!mf || !Vf || !S || !A) return set_err(EKS_ERR_ARG, "eks_backward: NULL input");
+  if (B < 0 || T < 1) return set_err(EKS_ERR_ARG, "eks_backward: need B >= 0, T >= 1");
+  if (B == 0) return EKS_OK;
+  hipStream_t s = (hipStream_t)stream;
+  return dispatch_r(r, [&](auto Rc) {
+    constexpr int RR = decltype(Rc)::value;
+    hipLaunchKernelGGL((k_backward<RR>), dim3(grid_for(B, 64)), dim3(64), 0, s, B, T, mf, Vf, S,
+                       A, params_shared, ms, Vs, CV, status);
+    return check_launch("k_backward");
+  });
+}
+
+int eks_kalman_dot(int n, int r, int k, const double *x, const double *V, const double *C,
+                   const double *R, double *out, int32_t *status, void *stream) {
+  g_err.clear();
+  if (!x || !V || !C || !R || !out) return set_err(EKS_ERR_ARG, "eks_kalman_dot: NULL pointer");
+  if (k < 1) return set_err(EKS_ERR_ARG, "eks_kalman_dot: k must be >= 1");
+  hipStream_t s = (hipStream_t)stream;
+  return dispatch_r(r, [&](auto Rc) {
+    return dispatch_n(n, [&](auto Nc) {
+      constexpr int RR = decltype(Rc)::value, NN = decltype(Nc)::value;
+      hipLaunchKernelGGL((k_kalman_dot<RR, NN>), dim3(1), dim3(64), 0, s, k, x, V, C, R, out,
+                         status);
+      return check_launch("k_kalman_dot");
+    });
+  });
+}
+
+}  // extern "C"

@@ -1,0 +1,150 @@
+// Ensemble reduction over E members (eks/ensemble_kalman.py:34-46), in
+// registers.  Matches numpy's arithmetic:
+//   mean = pairwise_sum(x) / E                     (numpy add.reduce order)
+//   var  = sum((x - mean)^2) / E / E               (np.var ddof=0, then / E)
+//   median: middle order statistic, or (lo + hi) / 2 for even E
+// and propagates NaN as np.median / np.var do.
+#pragma once
+#include "small_linalg.hpp"
+
+namespace eks {
+
+template <typename T>
+EKS_DEV double to_f64(T v) { return static_cast<double>(v); }
+
+// numpy-order summation of a register array: numpy's pairwise_sum rule for
+// n <= 128 (sequential below 8 elements, 8 interleaved partial sums above).
+template <int E>
+EKS_DEV double np_sum(const double (&x)[E]) {
+  if constexpr (E < 8) {
+    double s = x[0];
+#pragma unroll
+    for (int i = 1; i < E; ++i) s += x[i];
+    return s;
+  } else {
+    double r[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = x[j];
+    constexpr int full = E - (E % 8);
+#pragma unroll
+    for (int i = 8; i < full; i += 8)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) r[j] += x[i + j];
+    double s = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+#pragma unroll
+    for (int k = full; k < E; ++k) s += x[k];
+    return s;
+  }
+}
+
+// Sorting network (odd-even transposition) on E values of the input type:
+// min/max on the raw member values is exact, the median is converted after.
+template <int E, typename T>
+EKS_DEV void sort_net(T (&v)[E]) {
+#pragma unroll
+  for (int p = 0; p < E; ++p)
+#pragma unroll
+    for (int i = p & 1; i + 1 < E; i += 2) {
+      const T a = v[i], b = v[i + 1];
+      v[i] = a < b ? a : b;
+      v[i + 1] = a < b ? b : a;
+    }
+}
+
+// Reduce one column of E member values (compile-time E).
+template <int E, typename T>
+EKS_DEV void ensemble_reduce(const T (&raw)[E], bool median, double &avg, double &var) {
+  double x[E];
+  bool has_nan = false;
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    x[e] = to_f64(raw[e]);
+    has_nan |= (x[e] != x[e]);
+  }
+  const double mean = np_sum<E>(x) / E;
+  double d[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const double t = x[e] - mean;
+    d[e] = t * t;
+  }
+  var = np_sum<E>(d) / E / E;
+  if (median) {
+    T s[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) s[e] = raw[e];
+    sort_net<E, T>(s);
+    if constexpr (E % 2 == 1) {
+      avg = to_f64(s[E / 2]);
+    } else {
+      avg = (to_f64(s[E / 2 - 1]) + to_f64(s[E / 2])) / 2.0;
+    }
+  } else {
+    avg = mean;
+  }
+  if (has_nan) {
+    avg = __builtin_nan("");
+    var = __builtin_nan("");
+  }
+}
+
+// Runtime-E reduction (E up to EKS_MAX_MEMBERS) reading members straight from
+// memory: O(E^2) rank selection for the median.  Used only when E has no
+// compiled-in specialisation.
+template <typename T>
+EKS_DEV void ensemble_reduce_rt(const T *p, long long se, int E, bool median, double &avg,
+                                double &var) {
+  bool has_nan = false;
+  // numpy pairwise_sum order over f(0..E-1)
+  auto np_sum_rt = [&](auto f) {
+    if (E < 8) {
+      double s = f(0);
+      for (int i = 1; i < E; ++i) s += f(i);
+      return s;
+    }
+    double r[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = f(j);
+    const int full = E - (E % 8);
+    for (int i = 8; i < full; i += 8)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) r[j] += f(i + j);
+    double s = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (int k = full; k < E; ++k) s += f(k);
+    return s;
+  };
+  const double mean = np_sum_rt([&](int i) { return to_f64(p[(long long)i * se]); }) / E;
+  var = np_sum_rt([&](int i) {
+          const double t = to_f64(p[(long long)i * se]) - mean;
+          return t * t;
+        }) / E / E;
+  for (int e = 0; e < E; ++e) {
+    const double v = to_f64(p[(long long)e * se]);
+    has_nan |= (v != v);
+  }
+  if (median) {
+    // order statistics k_lo, k_hi (equal for odd E)
+    const int k_hi = E / 2, k_lo = (E % 2) ? E / 2 : E / 2 - 1;
+    double v_lo = 0.0, v_hi = 0.0;
+    for (int i = 0; i < E; ++i) {
+      const T xi = p[(long long)i * se];
+      int less = 0, eq = 0;
+      for (int j = 0; j < E; ++j) {
+        const T xj = p[(long long)j * se];
+        less += (xj < xi);
+        eq += (xj == xi);
+      }
+      if (less <= k_lo && k_lo < less + eq) v_lo = to_f64(xi);
+      if (less <= k_hi && k_hi < less + eq) v_hi = to_f64(xi);
+    }
+    avg = (E % 2) ? v_hi : (v_lo + v_hi) / 2.0;
+  } else {
+    avg = mean;
+  }
+  if (has_nan) {
+    avg = __builtin_nan("");
+    var = __builtin_nan("");
+  }
+}
+
+}  // namespace eks

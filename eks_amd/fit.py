@@ -1,0 +1,163 @@
+"""Model fitting that precedes the smoother (host side, per keypoint).
+
+These are the steps the reference's wrappers run between ``ensemble`` and
+``filtering_pass``.  They reduce over
+the time axis once per trajectory and are small next to the recursions;
+the recursions themselves run in the HIP kernels.
+
+    singleview_model   build definition
+    multicam_model     eks/multiview_pca_smoother.py:684-731
+    pupil_model        eks/pupil_smoother.py:101-172
+"""
+from __future__ import annotations
+
+import warnings
+
+import numpy as np
+
+PUPIL_KEYS = ('pupil_top_r_x', 'pupil_top_r_y', 'pupil_bottom_r_x', 'pupil_bottom_r_y',
+              'pupil_right_r_x', 'pupil_right_r_y', 'pupil_left_r_x', 'pupil_left_r_y')
+# measurement matrix of eks/pupil_smoother.py:150-153 (rows in PUPIL_KEYS order)
+PUPIL_C = np.array([[0, 1, 0], [-.5, 0, 1], [0, 1, 0], [.5, 0, 1],
+                    [.5, 1, 0], [0, 0, 1], [-.5, 1, 0], [0, 0, 1]], dtype=np.float64)
+
+
+def low_variance_frames(ens_vars: np.ndarray, quantile_keep: float) -> np.ndarray:
+    """Indices of frames whose largest ensemble variance is at or below the
+    ``quantile_keep`` percentile (linear interpolation), as
+    eks/multiview_pca_smoother.py:685-688."""
+    worst = ens_vars.max(axis=1)
+    return np.flatnonzero(worst <= np.percentile(worst, quantile_keep))
+
+
+def _step_cov(z_good: np.ndarray, smooth_param: float) -> np.ndarray:
+    """Q = s * cov(successive differences of the kept frames), ddof = 1
+    (eks/multiview_pca_smoother.py:726-728)."""
+    d = np.diff(z_good, axis=0)
+    return smooth_param * np.atleast_2d(np.cov(d.T))
+
+
+def singleview_model(preds, ens_vars, smooth_param, quantile_keep):
+    """Single-view parameterisation: the multicam template
+    without PCA -- C = A = I2, m0 = 0, S0 = diag(var of kept frames),
+    Q = s cov(diff(kept frames)), offset = mean of kept frames."""
+    keep = low_variance_frames(ens_vars, quantile_keep)
+    offset = preds[keep].mean(axis=0)
+    z = preds[keep] - offset
+    return dict(m0=np.zeros(2), S0=np.diag(z.var(axis=0)), A=np.eye(2),
+                Q=_step_cov(z, smooth_param), C=np.eye(2), offset=offset, keep=keep)
+
+
+def principal_axes(X: np.ndarray, k: int):
+    """Top-k principal axes of the rows of X (eigen-decomposition of the
+    sample covariance, as sklearn's PCA 'covariance_eigh' solver).  Row i of
+    the result is axis i; signs are arbitrary (outputs do not depend on them
+    because S0 is diagonal)."""
+    Xc = X - X.mean(axis=0)
+    w, v = np.linalg.eigh(Xc.T @ Xc / max(len(X) - 1, 1))
+    top = np.argsort(w)[::-1][:k]
+    return v[:, top].T, X.mean(axis=0)
+
+
+def multicam_model(preds, ens_vars, smooth_param, quantile_keep, n_latent=3):
+    """eks/multiview_pca_smoother.py:684-731 for one keypoint seen by V
+    cameras: preds / ens_vars are (T, 2V) (camera-major x, y columns)."""
+    keep = low_variance_frames(ens_vars, quantile_keep)
+    offset = preds[keep].mean(axis=0)
+    y = preds - offset
+    axes, centre = principal_axes(y[keep], n_latent)
+    z_keep = (y[keep] - centre) @ axes.T
+    r = n_latent
+    return dict(m0=np.zeros(r), S0=np.diag(z_keep.var(axis=0)), A=np.eye(r),
+                Q=_step_cov(z_keep, smooth_param), C=axes.T.copy(), offset=offset, keep=keep)
+
+
+def pupil_centre(cols) -> np.ndarray:
+    """Pupil centre of mass from the four keypoints (eks/pupil_smoother.py:14-39)."""
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore", category=RuntimeWarning)
+        top = np.stack([cols['pupil_top_r_x'], cols['pupil_top_r_y']], 1)
+        bot = np.stack([cols['pupil_bottom_r_x'], cols['pupil_bottom_r_y']], 1)
+        lef = np.stack([cols['pupil_left_r_x'], cols['pupil_left_r_y']], 1)
+        rig = np.stack([cols['pupil_right_r_x'], cols['pupil_right_r_y']], 1)
+        x_tb = np.nanmedian(np.stack([top[:, 0], bot[:, 0]], 1), axis=1)   # either may be NaN
+        x_lr = np.median(np.stack([rig[:, 0], lef[:, 0]], 1), axis=1)      # both needed
+        y_tb = np.median(np.stack([top[:, 1], bot[:, 1]], 1), axis=1)      # both needed
+        y_lr = np.nanmedian(np.stack([rig[:, 1], lef[:, 1]], 1), axis=1)   # either may be NaN
+        return np.stack([np.nanmedian(np.stack([x_tb, x_lr], 1), axis=1),
+                         np.nanmedian(np.stack([y_tb, y_lr], 1), axis=1)], 1)
+
+
+def pupil_diameter(cols) -> np.ndarray:
+    """Median of six diameter estimates: top-bottom, left-right and four
+    neighbour pairs scaled by sqrt 2 (eks/pupil_smoother.py:42-68)."""
+    p = {k: np.stack([cols[f'pupil_{k}_r_x'], cols[f'pupil_{k}_r_y']])
+         for k in ('top', 'bottom', 'left', 'right')}
+    ests = [np.linalg.norm(p['top'] - p['bottom'], axis=0),
+            np.linalg.norm(p['left'] - p['right'], axis=0)]
+    ests += [np.linalg.norm(p[a] - p[b], axis=0) * 2 ** 0.5
+             for a, b in (('top', 'left'), ('top', 'right'), ('bottom', 'left'), ('bottom', 'right'))]
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore", category=RuntimeWarning)
+        return np.nanmedian(ests, axis=0)
+
+
+def pupil_model(preds, state_transition_matrix):
+    """eks/pupil_smoother.py:109-172: latent (diameter, com_x, com_y)."""
+    A = np.asarray(state_transition_matrix, dtype=np.float64)
+    cols = {k: preds[:, j] for j, k in enumerate(PUPIL_KEYS)}
+    com = pupil_centre(cols)
+    diam = pupil_diameter(cols)
+    mx, my = com[:, 0].mean(), com[:, 1].mean()
+    var = np.array([diam.var(), (com[:, 0] - mx).var(), (com[:, 1] - my).var()])
+    return dict(m0=np.array([diam.mean(), 0.0, 0.0]), S0=np.diag(var), A=A,
+                Q=np.diag(var * (1 - np.diag(A) ** 2)), C=PUPIL_C.copy(),
+                offset=np.array([mx, my] * 4), mx=mx, my=my)
+
+
+# --------------------------------------------------------------------------
+# batched single-view fit on device tensors (B trajectories at once)
+# --------------------------------------------------------------------------
+def _np_percentile_linear(x_sorted, q):
+    """np.percentile(..., q) 'linear' on rows of an ascending-sorted (B, T)
+    tensor: virtual index (T-1) q/100 and numpy's _lerp."""
+    T = x_sorted.shape[1]
+    vi = (T - 1) * (q / 100.0)
+    lo = int(np.floor(vi))
+    hi = min(lo + 1, T - 1)
+    g = vi - lo
+    a = x_sorted[:, lo]
+    b = x_sorted[:, hi]
+    d = b - a
+    return b - d * (1 - g) if g >= 0.5 else a + d * g
+
+
+def singleview_model_batch(preds, ens_vars, smooth_param, quantile_keep):
+    """Batched singleview_model on (B, T, 2) float64 CUDA tensors (preds /
+    ensemble variances as returned by eks_ensemble).  Returns a dict of
+    (B, ...) tensors (m0, S0, A, Q, C, offset)."""
+    import torch
+    B, T, n = preds.shape
+    worst = ens_vars.max(dim=2).values
+    thr = _np_percentile_linear(torch.sort(worst, dim=1).values, quantile_keep)
+    keep = worst <= thr[:, None]                              # (B, T)
+    cnt = keep.sum(dim=1).to(preds.dtype)                     # (B,)
+    offset = (preds * keep[..., None]).sum(dim=1) / cnt[:, None]
+    z = (preds - offset[:, None, :]) * keep[..., None]
+    zm = z.sum(dim=1) / cnt[:, None]
+    S0 = torch.diag_embed((((preds - offset[:, None, :] - zm[:, None, :]) ** 2)
+                           * keep[..., None]).sum(dim=1) / cnt[:, None])
+    # successive differences between consecutive KEPT frames
+    idx = torch.arange(T, device=preds.device).expand(B, T)
+    last = torch.where(keep, idx, torch.full_like(idx, -1)).cummax(dim=1).values
+    prev = torch.cat([torch.full_like(last[:, :1], -1), last[:, :-1]], dim=1)
+    pair = keep & (prev >= 0)
+    prev_c = prev.clamp(min=0)
+    d = preds - torch.gather(preds, 1, prev_c[..., None].expand(B, T, n))
+    npair = pair.sum(dim=1).to(preds.dtype)
+    dm = (d * pair[..., None]).sum(dim=1) / npair[:, None]
+    dc = (d - dm[:, None, :]) * pair[..., None]
+    Q = smooth_param * torch.einsum('bti,btj->bij', dc, dc) / (npair - 1)[:, None, None]
+    eye = torch.eye(n, dtype=preds.dtype, device=preds.device).expand(B, n, n)
+    return dict(m0=torch.zeros(B, n, dtype=preds.dtype, device=preds.device), S0=S0,
+                A=eye.clone(), Q=Q, C=eye.clone(), offset=offset)

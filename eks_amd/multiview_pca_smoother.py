@@ -1,0 +1,3 @@
+"""Module-path alias of the reference's eks/multiview_pca_smoother.py."""
+from .core import ensemble, filtering_pass, kalman_dot, smooth_backward  # noqa: F401
+from .smoothers import ensemble_kalman_smoother_multi_cam  # noqa: F401

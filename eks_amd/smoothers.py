@@ -1,0 +1,114 @@
+"""Per-keypoint entry points, API-compatible with the reference wrappers.
+
+    ensemble_kalman_smoother_multi_cam   eks/multiview_pca_smoother.py:611-767
+    ensemble_kalman_smoother_pupil       eks/pupil_smoother.py:82-223
+    ensemble_kalman_smoother_single_view build definition
+
+Flow for one keypoint: member DataFrames -> (E, T, n) array -> GPU ensemble
+(eks_ensemble) -> host model fit (eks_amd.fit) -> GPU fused smoother
+(eks_smooth: ensemble, forward, backward, projection) -> DataFrames in the
+reference's output format.  No step of the smoother runs on the CPU.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pandas as pd
+
+from . import _lib, batch, core, fit
+from .utils import TRACKER, make_dlc_pandas_index
+
+
+def _run_fused(stack: np.ndarray, model: dict, mode: str = "median", want_ms=False,
+               want_nll=False):
+    """stack (E, T, n) float64 host array + model -> out (T, n), ms, nll."""
+    torch = _lib.require_gpu()
+    E, T, n = stack.shape
+    r = len(model["m0"])
+    obs = torch.from_numpy(np.ascontiguousarray(stack, dtype=np.float64)).to("cuda")
+    obs = obs.permute(1, 0, 2).unsqueeze(0)  # (1, T, E, n) view, no copy
+    params = batch.pack_params(model["m0"], model["S0"], model["A"], model["Q"], model["C"],
+                               model["offset"])
+    res = batch.smooth(obs, params, n=n, r=r, mode=mode, want_ms=want_ms, want_nll=want_nll)
+    if bool((res["status"] != 0).any().item()):
+        raise np.linalg.LinAlgError("Singular matrix")
+    out = res["out"][0].cpu().numpy()
+    ms = res["ms"][0].cpu().numpy() if want_ms else None
+    nll = float(res["nll"][0].item()) if want_nll else None
+    return out, ms, nll
+
+
+def ensemble_kalman_smoother_multi_cam(markers_list_cameras, keypoint_ensemble, smooth_param,
+                                       quantile_keep_pca, camera_names):
+    """Multi-view PCA smoother for one keypoint (eks/multiview_pca_smoother.py:611-767).
+
+    markers_list_cameras[camera][model] is a DataFrame whose first two
+    columns are that camera's x and y predictions.  Returns
+    {f'{camera}_df': DataFrame} with (scorer, keypoint, x/y/likelihood)
+    columns; likelihood is NaN as in the reference."""
+    V = len(camera_names)
+    if V < 2:
+        raise ValueError("ensemble_kalman_smoother_multi_cam needs at least two cameras "
+                         "(the reference's 3-component PCA needs >= 3 columns); use "
+                         "ensemble_kalman_smoother_single_view for one view")
+    n_models = len(markers_list_cameras[0])
+    cols = [np.stack([np.asarray(markers_list_cameras[c][e].to_numpy()[:, :2], dtype=np.float64)
+                      for e in range(n_models)]) for c in range(V)]  # V x (E, T, 2)
+    stack = np.concatenate(cols, axis=2)  # (E, T, 2V), camera-major columns
+    preds, ev = core.ensemble_array(stack)
+    model = fit.multicam_model(preds, ev, smooth_param, quantile_keep_pca)
+    out, _, _ = _run_fused(stack, model)
+    pdindex = make_dlc_pandas_index([keypoint_ensemble])
+    dfs = {}
+    nan = np.full(out.shape[0], np.nan)
+    for c, cam in enumerate(camera_names):
+        arr = np.stack([out[:, 2 * c], out[:, 2 * c + 1], nan], axis=1)
+        dfs[cam + "_df"] = pd.DataFrame(arr, columns=pdindex)
+    return dfs
+
+
+def ensemble_kalman_smoother_pupil(markers_list, keypoint_names, tracker_name,
+                                   state_transition_matrix):
+    """IBL pupil smoother (eks/pupil_smoother.py:82-223).
+
+    Returns {'markers_df': smoothed keypoints in the order top, right, bottom,
+    left (NaN likelihood), 'latents_df': diameter, com_x, com_y}."""
+    stack = np.stack([np.stack([np.asarray(df[k], dtype=np.float64) for k in fit.PUPIL_KEYS], 1)
+                      for df in markers_list])  # (E, T, 8)
+    preds, _ = core.ensemble_array(stack)
+    model = fit.pupil_model(preds, state_transition_matrix)
+    out, ms, _ = _run_fused(stack, model, want_ms=True)
+    by_key = {k: out[:, j] for j, k in enumerate(fit.PUPIL_KEYS)}
+    nan = np.full(out.shape[0], np.nan)
+    cols = []
+    for kp in ('top', 'right', 'bottom', 'left'):  # output order of :199-203
+        cols += [by_key[f'pupil_{kp}_r_x'], by_key[f'pupil_{kp}_r_y'], nan]
+    markers_df = pd.DataFrame(np.stack(cols, 1), columns=make_dlc_pandas_index(keypoint_names))
+    lat = np.stack([ms[:, 0], ms[:, 1] + model["mx"], ms[:, 2] + model["my"]], 1)
+    idx = pd.MultiIndex.from_arrays([[tracker_name] * 3, ['diameter', 'com_x', 'com_y']],
+                                    names=('scorer', 'latent'))
+    return {'markers_df': markers_df, 'latents_df': pd.DataFrame(lat, columns=idx)}
+
+
+def ensemble_kalman_smoother_single_view(markers_list, keypoint_ensemble, smooth_param,
+                                         quantile_keep_pca=25, ensembling_mode="median"):
+    """Single-view EKS for one keypoint (the reference
+    snapshot has no single-view smoother).
+
+    markers_list: E DataFrames with '{keypoint}_x' / '{keypoint}_y' columns.
+    Model: C = A = I2, m0 = 0, S0 = diag(var), Q = s cov(diff) over the
+    low-variance frames, offset = their mean.  Returns {'markers_df',
+    'nll'} with the reference's output format."""
+    keys = [f"{keypoint_ensemble}_x", f"{keypoint_ensemble}_y"]
+    stack = np.stack([np.stack([np.asarray(df[k], dtype=np.float64) for k in keys], 1)
+                      for df in markers_list])  # (E, T, 2)
+    preds, ev = core.ensemble_array(stack, ensembling_mode)
+    model = fit.singleview_model(preds, ev, smooth_param, quantile_keep_pca)
+    out, _, nll = _run_fused(stack, model, mode=ensembling_mode, want_nll=True)
+    nan = np.full(out.shape[0], np.nan)
+    df = pd.DataFrame(np.stack([out[:, 0], out[:, 1], nan], 1),
+                      columns=make_dlc_pandas_index([keypoint_ensemble]))
+    return {'markers_df': df, 'nll': nll}
+
+
+__all__ = ["ensemble_kalman_smoother_multi_cam", "ensemble_kalman_smoother_pupil",
+           "ensemble_kalman_smoother_single_view", "TRACKER"]

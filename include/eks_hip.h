@@ -1,0 +1,157 @@
+/*
+ * eks_hip.h -- C ABI of libeks_hip.so, the MI355X (gfx950) ensemble Kalman
+ * smoother.  Plain pointers and sizes only: no torch or numpy types.
+ *
+ * The reference (erialc-cal/eks, Python) has no FFI; its boundary is the four
+ * Python functions of eks/ensemble_kalman.py.  Each entry point below states
+ * which of them it replaces.  The Python package eks_amd binds these symbols
+ * with ctypes (see INTEGRATION.md for the binding a maintainer of the
+ * reference would add).
+ *
+ * Conventions
+ *   - Every array argument is a DEVICE pointer (hipMalloc'd / torch cuda
+ *     memory) unless the comment says otherwise.  Calls are stream-ordered on
+ *     `stream` (a hipStream_t passed as void*; NULL = the null stream) and do
+ *     not synchronise; they never allocate, so they can be captured in a
+ *     hipGraph.
+ *   - Floating point is float64 ("f64") throughout the recursions; member
+ *     observations may be f32 or f64 (EKS_F32 / EKS_F64).
+ *   - Matrices are row-major.  Batched arrays carry a leading trajectory
+ *     index b in [0, B); a "trajectory" is one (video, keypoint) series.
+ *   - Return value: EKS_OK or an error code; eks_last_error() gives the text
+ *     (thread-local).  Numerical failures are reported per trajectory in the
+ *     optional int32 `status` array (device, length B):
+ *       0 = ok, EKS_SINGULAR = a matrix the reference would hand to
+ *       np.linalg.solve was singular (the reference raises LinAlgError).
+ *     NaNs propagate exactly as in numpy and are not an error.
+ */
+#ifndef EKS_HIP_H
+#define EKS_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  EKS_OK = 0,
+  EKS_ERR_ARG = 1,         /* bad size / NULL pointer / bad mode */
+  EKS_ERR_UNSUPPORTED = 2, /* (r, n, E) combination not compiled in */
+  EKS_ERR_HIP = 4,         /* a HIP runtime call failed */
+  EKS_SINGULAR = 3         /* per-trajectory status value */
+};
+
+enum { EKS_F32 = 0, EKS_F64 = 1 };
+enum { EKS_MEDIAN = 0, EKS_MEAN = 1 };
+
+/* Last error message of the calling thread ("" if none). */
+const char *eks_last_error(void);
+
+/* Library ABI version (major*100 + minor). */
+int eks_version(void);
+
+/* Largest state / observation / ensemble sizes the kernels accept. */
+int eks_max_latent(void);
+int eks_max_obs(void);
+int eks_max_members(void);
+
+/*
+ * eks_ensemble -- replaces eks/ensemble_kalman.py:4-57 `ensemble()`.
+ *
+ * Member observation x(b, t, e, j) is read from
+ *     obs[b*sb + t*st + e*se + j*sj]      (strides in ELEMENTS, any layout)
+ * for b < B, t < T, e < E, j < n.  For every (b, t, j):
+ *     preds = median_e x   (mode EKS_MEDIAN; mean of the two middle values
+ *                            for even E, as np.median)  or  mean_e x
+ *     vars  = var_e(x, ddof=0) / E     (in both modes, quirk of :46)
+ * A NaN among the members makes both outputs NaN (np.median / np.var).
+ * preds / vars: (B, T, n) contiguous f64.
+ */
+int eks_ensemble(const void *obs, int obs_dtype, int64_t B, int64_t T, int E, int n,
+                 int64_t sb, int64_t st, int64_t se, int64_t sj, int mode,
+                 double *preds, double *vars, void *stream);
+
+/*
+ * eks_forward -- replaces eks/ensemble_kalman.py:59-107 `filtering_pass()`
+ * (and the kalman_dot calls it makes, :110-117), batched over B trajectories.
+ *
+ * Inputs (all f64, contiguous):
+ *   y  (B, T, n)   observations        ev (B, T, n)  ensemble variances
+ *   m0 (B, r)      S0 (B, r, r)        A (B, r, r)   Q (B, r, r)   C (B, n, r)
+ *   R  (B, n, n) or NULL: the caller's R matrix.  As in the reference its
+ *      diagonal is replaced by ev[t] at every step; NULL means R is diagonal.
+ *      This function does not write R (the Python shim reproduces the
+ *      in-place mutation on the host).
+ *   params_shared: if nonzero, m0/S0/A/Q/C/R hold ONE trajectory's values
+ *      used for all b (batch stride 0).
+ * Outputs (any may be NULL):
+ *   mf (B, T, r)   Vf (B, T, r, r)   S (B, T, r, r) -- S[t] = A Vf[t] A^T + Q,
+ *      the covariance predicted for step t+1; S[T-1] = 0 as in the reference.
+ *   nll (B) -- the Gaussian innovation negative log-likelihood
+ *      (the reference has no counterpart).
+ *   status (B) int32 -- see above.
+ */
+int eks_forward(int64_t B, int64_t T, int n, int r, const double *y, const double *ev,
+                const double *m0, const double *S0, const double *A, const double *Q,
+                const double *C, const double *R, int params_shared, double *mf, double *Vf,
+                double *S, double *nll, int32_t *status, void *stream);
+
+/*
+ * eks_backward -- replaces eks/ensemble_kalman.py:120-164 `smooth_backward()`.
+ *   mf (B,T,r), Vf (B,T,r,r), S (B,T,r,r), A (B,r,r) (shared if params_shared)
+ *   -> ms (B,T,r), Vs (B,T,r,r), CV (B,T-1,r,r); any output may be NULL.
+ * J_t = solve(S[t], A Vf[t])^T, exactly as :158 (Q, C and y are unused by
+ * the reference and are not arguments here).
+ */
+int eks_backward(int64_t B, int64_t T, int r, const double *mf, const double *Vf,
+                 const double *S, const double *A, int params_shared, double *ms, double *Vs,
+                 double *CV, int32_t *status, void *stream);
+
+/*
+ * eks_kalman_dot -- replaces eks/ensemble_kalman.py:110-117 `kalman_dot()`:
+ *   out (r, k) = V C^T (R + C V C^T)^{-1} x,  x (n, k), V (r, r), C (n, r), R (n, n).
+ * k = 1 for the vector form.  Single problem, f64.
+ */
+int eks_kalman_dot(int n, int r, int k, const double *x, const double *V, const double *C,
+                   const double *R, double *out, int32_t *status, void *stream);
+
+/*
+ * Packed per-trajectory model for the fused smoother: for each b, P doubles
+ *   [ m0 (r) | S0 (r*r) | A (r*r) | Q (r*r) | C (n*r) | offset (n) ]
+ * with P = eks_param_len(n, r).  `offset` is added to C ms[t] on output (the
+ * camera / keypoint means the wrappers subtract before filtering and add back
+ * after: eks/multiview_pca_smoother.py:698-700, :756-765;
+ * eks/pupil_smoother.py:158-172, :197).
+ */
+int64_t eks_param_len(int n, int r);
+
+/*
+ * eks_smooth -- the fused hot path: ensemble (eks_ensemble) -> centre
+ * (y = preds - offset) -> forward filter -> RTS backward -> projection
+ * out = C ms + offset, i.e. eks/ensemble_kalman.py:4-164 plus
+ * eks/multiview_pca_smoother.py:745 / eks/pupil_smoother.py:190, in one call
+ * for B trajectories with R diagonal (R_t = diag(ev[t])).
+ *
+ *   obs      member observations, strides as eks_ensemble
+ *   params   (B, P) f64 packed models (see eks_param_len)
+ *   out      smoothed observations out(b,t,j) = out[b*ob + t*ot + j*oj] (f64)
+ *   ms       (B, T, r) contiguous smoothed latents, or NULL
+ *   nll      (B) or NULL
+ *   workspace / workspace_bytes: device scratch of at least
+ *            eks_smooth_workspace_bytes(...) bytes (not zeroed by caller).
+ *   algo     0 = automatic, 1 = sequential (one lane per trajectory),
+ *            2 = time-parallel chunked scan
+ */
+size_t eks_smooth_workspace_bytes(int64_t B, int64_t T, int n, int r, int algo);
+int eks_smooth(const void *obs, int obs_dtype, int64_t B, int64_t T, int E, int n, int r,
+               int64_t sb, int64_t st, int64_t se, int64_t sj, int mode, const double *params,
+               double *out, int64_t ob, int64_t ot, int64_t oj, double *ms, double *nll,
+               void *workspace, size_t workspace_bytes, int algo, int32_t *status,
+               void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* EKS_HIP_H */

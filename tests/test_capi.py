@@ -1,0 +1,60 @@
+"""CPU-side checks of the C ABI: the library loads, exports exactly what
+include/eks_hip.h declares, and rejects bad arguments before touching the
+GPU.  No kernel is launched here (there is no GPU in the build container)."""
+import ctypes
+
+import pytest
+
+from eks_amd import _lib
+
+
+def test_library_exports_every_header_symbol():
+    lib = _lib.load()
+    declared = _lib.header_symbols()
+    assert len(declared) >= 10
+    for name in declared:
+        assert hasattr(lib, name), f"{name} declared in include/eks_hip.h but not exported"
+    # and the ctypes signature table covers every declared symbol
+    assert set(declared) == set(_lib.SIGNATURES)
+
+
+def test_limits_and_sizes():
+    lib = _lib.load()
+    assert lib.eks_version() >= 100
+    assert lib.eks_max_latent() >= 3 and lib.eks_max_obs() >= 8 and lib.eks_max_members() >= 8
+    for n, r in [(2, 2), (8, 3), (4, 3)]:
+        assert lib.eks_param_len(n, r) == r + 3 * r * r + n * r + n
+    assert lib.eks_smooth_workspace_bytes(10, 100, 2, 2, 1) >= 10 * 100 * 5 * 8
+
+
+def test_argument_errors_do_not_launch():
+    lib = _lib.load()
+    rc = lib.eks_smooth(None, 0, 1, 10, 5, 2, 2, 0, 0, 0, 0, 0, None, None, 0, 0, 0,
+                        None, None, None, 0, 0, None, None)
+    assert rc == _lib.EKS_ERR_ARG
+    assert b"NULL" in lib.eks_last_error()
+    rc = lib.eks_ensemble(ctypes.c_void_p(8), 0, 1, 10, 5, 2, 0, 0, 0, 0, 7,
+                          ctypes.c_void_p(8), ctypes.c_void_p(8), None)
+    assert rc == _lib.EKS_ERR_ARG and b"averaging not supported" in lib.eks_last_error()
+    with pytest.raises(_lib.EksError):
+        _lib.check(rc, "eks_ensemble")
+
+
+def test_product_path_fails_loudly_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    import numpy as np
+    from eks_amd import core
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        core.filtering_pass(np.zeros((3, 2)), np.zeros(2), np.eye(2), np.eye(2), np.eye(2),
+                            np.eye(2), np.eye(2), np.ones((3, 2)))
+
+
+def test_product_package_never_imports_oracle():
+    import glob
+    import os
+    root = os.path.dirname(_lib.HERE)
+    for path in glob.glob(os.path.join(root, "eks_amd", "**", "*.py"), recursive=True):
+        src = open(path).read()
+        assert "oracle" not in src.replace("oracle/", ""), f"{path} references the oracle"

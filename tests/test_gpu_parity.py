@@ -1,0 +1,328 @@
+"""GPU parity: the HIP path (through the C ABI) against the golden vectors
+and the CPU oracle, on identical inputs.
+
+Tolerances: the recursions are float64 in both paths but use different
+(algebraically identical) update orders, so intermediates agree to ~1e-12
+relative; outputs in pixel units are held to the north-star bound
+max|d| < 1e-5 (BASELINE.json) and in practice agree to ~1e-10.
+"""
+import glob
+import os
+
+import numpy as np
+import pandas as pd
+import pytest
+
+from tests.conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+OUT_TOL = 1e-5          # north-star tolerance on smoothed outputs (pixels)
+INT_RTOL = 1e-8         # intermediates (mf, Vf, S, ms, Vs, CV)
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+def _close(a, b, rtol=INT_RTOL, atol=None):
+    a = np.asarray(a)
+    b = np.asarray(b)
+    scale = max(1.0, float(np.nanmax(np.abs(b))) if b.size else 1.0)
+    np.testing.assert_allclose(a, b, rtol=rtol, atol=(atol if atol is not None else rtol * scale),
+                               equal_nan=True)
+
+
+# -------------------------------------------------------------------------
+ENS = sorted(glob.glob(os.path.join(GOLDEN, "ensemble_*.npz")))
+
+
+@pytest.mark.parametrize("path", ENS, ids=[os.path.basename(p)[:-4] for p in ENS])
+def test_ensemble_golden(torch, path):
+    from eks_amd import core
+    g = np.load(path)
+    mode = "median" if "median" in path else "mean"
+    p, v = core.ensemble_array(g["stack"], mode)
+    # selection and numpy-ordered sums: expected bit-exact
+    np.testing.assert_array_equal(np.isnan(p), np.isnan(g["preds"]))
+    np.testing.assert_allclose(p, g["preds"], rtol=0, atol=1e-12, equal_nan=True)
+    np.testing.assert_allclose(v, g["vars"], rtol=1e-14, atol=1e-14, equal_nan=True)
+
+
+def test_ensemble_dataframe_api(torch):
+    from eks_amd import core
+    g = np.load(os.path.join(GOLDEN, "ensemble_E5_median.npz"))
+    keys = ["a", "b", "c"]
+    dfs = [pd.DataFrame(g["stack"][e], columns=keys) for e in range(5)]
+    preds, var, stacks, avg_d, var_d, stack_d = core.ensemble(dfs, keys)
+    assert stacks.shape == g["stacks"].shape
+    np.testing.assert_array_equal(stacks, g["stacks"])
+    np.testing.assert_allclose(avg_d["b"], g["preds"][:, 1], atol=1e-12, equal_nan=True)
+    np.testing.assert_array_equal(stack_d[3]["c"], g["stack"][3, :, 2])
+    with pytest.raises(ValueError):
+        core.ensemble(dfs, keys, mode="max")
+
+
+@pytest.mark.parametrize("E", [1, 2, 3, 5, 7, 9, 16, 33])
+def test_ensemble_member_counts_vs_oracle(torch, E):
+    """Compiled (E <= 8) and runtime-E paths, float32 and float64 members."""
+    from eks_amd import _lib, core
+    from oracle import eks_oracle as O
+    rng = np.random.default_rng(E)
+    stack = rng.normal(200, 30, size=(E, 301, 4)).round(2)
+    stack[:, 5, 0] = 7.25  # ties
+    for mode in ("median", "mean"):
+        p, v = core.ensemble_array(stack, mode)
+        po, vo = O.ensemble_array(stack, mode)
+        np.testing.assert_allclose(p, po, rtol=0, atol=1e-12)
+        np.testing.assert_allclose(v, vo, rtol=1e-13, atol=1e-13)
+    # float32 members through the raw C ABI, trajectory-minor layout
+    B = 3
+    s32 = rng.normal(200, 30, size=(301, E, 4, B)).astype(np.float32)  # (T, E, n, B)
+    d = torch.from_numpy(s32).cuda()
+    preds = torch.empty((B, 301, 4), dtype=torch.float64, device="cuda")
+    var = torch.empty_like(preds)
+    lib = _lib.load()
+    _lib.check(lib.eks_ensemble(d.data_ptr(), _lib.EKS_F32, B, 301, E, 4, 1, E * 4 * B, 4 * B, B,
+                                _lib.EKS_MEDIAN, preds.data_ptr(), var.data_ptr(),
+                                _lib.stream_ptr()), "eks_ensemble")
+    for b in range(B):
+        po, vo = O.ensemble_array(np.transpose(s32[..., b], (1, 0, 2)).astype(np.float64))
+        np.testing.assert_allclose(preds[b].cpu().numpy(), po, rtol=0, atol=1e-12)
+        np.testing.assert_allclose(var[b].cpu().numpy(), vo, rtol=1e-13, atol=1e-13)
+
+
+# -------------------------------------------------------------------------
+CORE = sorted(glob.glob(os.path.join(GOLDEN, "core_*.npz")))
+
+
+@pytest.mark.parametrize("path", CORE, ids=[os.path.basename(p)[:-4] for p in CORE])
+def test_core_golden(torch, path):
+    """filtering_pass / smooth_backward / kalman_dot drop-ins vs the reference."""
+    from eks_amd import core
+    g = np.load(path)
+    R = g["R_in"].copy()
+    mf, Vf, S = core.filtering_pass(g["y"], g["m0"], g["S0"], g["C"], R, g["A"], g["Q"], g["ev"])
+    _close(mf, g["mf"])
+    _close(Vf, g["Vf"])
+    _close(S, g["S"])
+    np.testing.assert_array_equal(R, g["R_out"])  # in-place mutation reproduced
+    T = len(g["y"])
+    if T >= 2:
+        assert np.all(S[-1] == 0.0)
+    ms, Vs, CV = core.smooth_backward(g["y"], mf, Vf, S, g["A"], g["Q"], g["C"])
+    if T >= 2:
+        _close(ms, g["ms"])
+        _close(Vs, g["Vs"])
+        _close(CV, g["CV"])
+    assert CV.shape == (T - 1,) + g["A"].shape
+    kd = core.kalman_dot(g["kd_vec_in"], g["S0"], g["C"], np.diag(g["ev"][0]))
+    _close(kd, g["kd_vec"], rtol=1e-10)
+    kd = core.kalman_dot(g["kd_mat_in"], g["S0"], g["C"], np.diag(g["ev"][0]))
+    _close(kd, g["kd_mat"], rtol=1e-10)
+
+
+def test_full_R_off_diagonal_vs_oracle(torch):
+    """A non-diagonal caller R: off-diagonals are kept, diagonal replaced."""
+    from eks_amd import core
+    from oracle import eks_oracle as O
+    g = np.load(os.path.join(GOLDEN, "core_rand_r3_n4_T257.npz"))
+    R0 = np.eye(4) + 0.2 * (np.ones((4, 4)) - np.eye(4))
+    R1, R2 = R0.copy(), R0.copy()
+    a = core.filtering_pass(g["y"], g["m0"], g["S0"], g["C"], R1, g["A"], g["Q"], g["ev"])
+    b = O.filtering_pass(g["y"], g["m0"], g["S0"], g["C"], R2, g["A"], g["Q"], g["ev"])
+    for x, y in zip(a, b):
+        _close(x, y)
+    np.testing.assert_array_equal(R1, R2)
+
+
+def test_nll_vs_oracle(torch):
+    from eks_amd import core
+    from oracle import eks_oracle as O
+    for name in ("core_rand_r3_n8_T1000", "core_rand_r2_n2_T1000", "core_zero_var_r2_n2_T300"):
+        g = np.load(os.path.join(GOLDEN, name + ".npz"))
+        a = core.compute_nll(g["y"], g["m0"], g["S0"], g["C"], g["A"], g["Q"], g["ev"])
+        b = O.compute_nll(g["y"], g["m0"], g["S0"], g["C"], g["A"], g["Q"], g["ev"])
+        assert abs(a - b) <= 1e-9 * abs(b), (name, a, b)
+
+
+def test_singular_raises_linalgerror(torch):
+    from eks_amd import core
+    y = np.zeros((4, 2))
+    ev = np.zeros((4, 2))
+    with pytest.raises(np.linalg.LinAlgError):
+        core.filtering_pass(y, np.zeros(2), np.zeros((2, 2)), np.eye(2), np.eye(2), np.eye(2),
+                            np.zeros((2, 2)), ev)
+    with pytest.raises(np.linalg.LinAlgError):
+        core.smooth_backward(y, np.zeros((4, 2)), np.zeros((4, 2, 2)), np.zeros((4, 2, 2)),
+                             np.eye(2))
+
+
+def test_nan_propagates_like_numpy(torch):
+    from eks_amd import core
+    from oracle import eks_oracle as O
+    g = np.load(os.path.join(GOLDEN, "core_rand_r2_n2_T257.npz"))
+    y = g["y"].copy()
+    y[100, 1] = np.nan
+    a = core.filtering_pass(y, g["m0"], g["S0"], g["C"], np.eye(2), g["A"], g["Q"], g["ev"])
+    b = O.filtering_pass(y, g["m0"], g["S0"], g["C"], np.eye(2), g["A"], g["Q"], g["ev"])
+    np.testing.assert_array_equal(np.isnan(a[0]), np.isnan(b[0]))
+    _close(a[0][:100], b[0][:100])
+
+
+# -------------------------------------------------------------------------
+# fused hot path (eks_smooth)
+# -------------------------------------------------------------------------
+SV = sorted(glob.glob(os.path.join(GOLDEN, "singleview_*.npz")))
+
+
+@pytest.mark.parametrize("path", SV, ids=[os.path.basename(p)[:-4] for p in SV])
+@pytest.mark.parametrize("dtype", ["f64", "f32"])
+def test_fused_singleview_golden(torch, path, dtype):
+    """eks_smooth on the reference-generated single-view fixtures (model from
+    the fixture), members as float64 and as float32 (they are f32 values)."""
+    from eks_amd import batch
+    g = np.load(path)
+    obs = g["obs"]  # (E, T, 2)
+    E, T, _ = obs.shape
+    params = batch.pack_params(g["m0"], g["S0"], g["A"], g["Q"], g["C"], g["means"])
+    npdt = np.float64 if dtype == "f64" else np.float32
+    d = batch.make_time_major(obs[None], dtype=npdt)  # (1, T, E, 2) view
+    res = batch.smooth(d, params, n=2, r=2, want_ms=True, want_nll=True)
+    assert int(res["status"][0]) == 0
+    out = res["out"][0].cpu().numpy()
+    assert np.abs(out - g["out"]).max() < OUT_TOL
+    _close(res["ms"][0].cpu().numpy(), g["ms"], rtol=1e-8)
+
+
+def _oracle_smooth_batch(stacks, models, O):
+    outs = []
+    for st, m in zip(stacks, models):
+        preds, ev = O.ensemble_array(st)
+        y = preds - m["offset"]
+        R = np.eye(len(m["offset"]))
+        mf, Vf, S = O.filtering_pass(y, m["m0"], m["S0"], m["C"], R, m["A"], m["Q"], ev)
+        ms, _, _ = O.smooth_backward(y, mf, Vf, S, m["A"])
+        outs.append(ms @ m["C"].T + m["offset"])
+    return outs
+
+
+@pytest.mark.parametrize("r,n,E", [(2, 2, 5), (3, 4, 5), (3, 6, 4), (3, 8, 5), (2, 2, 11)])
+def test_fused_batch_vs_oracle(torch, r, n, E):
+    """B independent trajectories with different models and layouts."""
+    from eks_amd import batch, synthetic
+    from oracle import eks_oracle as O
+    rng = np.random.default_rng(100 * r + n)
+    B, T = 70, 400
+    if n == 2:
+        stacks = synthetic.singleview_obs(rng, E, T, K=B).transpose(2, 0, 1, 3)  # (B, E, T, 2)
+    else:
+        stacks = synthetic.multiview_obs(rng, n // 2, E, T, K=B).transpose(2, 0, 1, 3)
+    stacks = stacks.astype(np.float64)
+    models = []
+    for b in range(B):
+        preds, ev = O.ensemble_array(stacks[b])
+        if n == 2:
+            p = O.singleview_params(preds, ev, 0.05, 25)
+        else:
+            p = O.multicam_params(preds, ev, 0.05, 25)
+        p["offset"] = p["means"]
+        models.append(p)
+    params = batch.pack_params(np.stack([m["m0"] for m in models]),
+                               np.stack([m["S0"] for m in models]),
+                               np.stack([m["A"] for m in models]),
+                               np.stack([m["Q"] for m in models]),
+                               np.stack([m["C"] for m in models]),
+                               np.stack([m["offset"] for m in models]))
+    ref = _oracle_smooth_batch(list(stacks), models, O)
+    # time-major float32 layout (the bench layout)
+    d = batch.make_time_major(stacks, dtype=np.float32)
+    res = batch.smooth(d, params, n=n, r=r, want_nll=True)
+    out = res["out"].cpu().numpy()
+    assert (res["status"] == 0).all()
+    err = max(np.abs(out[b] - ref[b]).max() for b in range(B))
+    assert err < OUT_TOL, err
+    # trajectory-major float64 layout gives the same numbers
+    d64 = torch.from_numpy(np.ascontiguousarray(stacks.transpose(0, 2, 1, 3))).cuda()  # (B,T,E,n)
+    res2 = batch.smooth(d64, params, n=n, r=r, want_nll=True)
+    np.testing.assert_array_equal(res2["out"].cpu().numpy(), out)
+    # NLL per trajectory vs the oracle's definition
+    for b in (0, B // 2, B - 1):
+        preds, ev = O.ensemble_array(stacks[b])
+        m = models[b]
+        nll = O.compute_nll(preds - m["offset"], m["m0"], m["S0"], m["C"], m["A"], m["Q"], ev)
+        assert abs(float(res["nll"][b]) - nll) <= 1e-9 * abs(nll)
+
+
+def test_fused_edge_cases(torch):
+    """T = 1, T = 2, zero-variance frames (all members agree) and NaN members."""
+    from eks_amd import batch
+    from oracle import eks_oracle as O
+    rng = np.random.default_rng(7)
+    for T in (1, 2, 3, 64):
+        st = rng.normal(100, 5, size=(1, 4, T, 2))
+        st[0, :, 0, 0] = 42.0   # exact agreement -> R_00 = 0 at t = 0
+        m = dict(m0=np.zeros(2), S0=np.diag([30.0, 20.0]), A=np.eye(2),
+                 Q=np.array([[0.5, 0.1], [0.1, 0.4]]), C=np.eye(2), offset=np.array([100., 100.]))
+        params = batch.pack_params(m["m0"], m["S0"], m["A"], m["Q"], m["C"], m["offset"])
+        res = batch.smooth(batch.make_time_major(st), params, n=2, r=2)
+        ref = _oracle_smooth_batch([st[0]], [m], O)[0]
+        assert np.abs(res["out"][0].cpu().numpy() - ref).max() < OUT_TOL
+    st = rng.normal(100, 5, size=(1, 5, 50, 2))
+    st[0, 2, 20, 1] = np.nan
+    res = batch.smooth(batch.make_time_major(st), params, n=2, r=2)
+    out = res["out"][0].cpu().numpy()
+    ref = _oracle_smooth_batch([st[0]], [m], O)[0]
+    np.testing.assert_array_equal(np.isnan(out), np.isnan(ref))
+
+
+# -------------------------------------------------------------------------
+# entry points on the reference's own data (goldens committed by the reference)
+# -------------------------------------------------------------------------
+MC = sorted(glob.glob(os.path.join(GOLDEN, "multicam_*.npz")))
+
+
+@pytest.mark.parametrize("path", MC, ids=[os.path.basename(p)[:-4] for p in MC])
+def test_multicam_entry_point_golden(torch, path):
+    from eks_amd.multiview_pca_smoother import ensemble_kalman_smoother_multi_cam
+    g = np.load(path)
+    stacks = g["stacks"]  # (V, E, T, 2)
+    V, E = stacks.shape[:2]
+    cams = [f"cam{c}" for c in range(V)]
+    by_cam = [[pd.DataFrame(stacks[c, e], columns=["x", "y"]) for e in range(E)]
+              for c in range(V)]
+    dfs = ensemble_kalman_smoother_multi_cam(by_cam, "kp", float(g["s"]), float(g["q"]), cams)
+    out = np.concatenate([dfs[f"{c}_df"].to_numpy()[:, :2] for c in cams], axis=1)
+    assert np.abs(out - g["golden"]).max() < OUT_TOL
+    assert np.abs(out - g["out"]).max() < OUT_TOL
+    assert np.isnan(dfs["cam0_df"].to_numpy()[:, 2]).all()
+
+
+def test_pupil_entry_point_golden(torch):
+    from eks_amd.pupil_smoother import ensemble_kalman_smoother_pupil
+    from eks_amd.fit import PUPIL_KEYS
+    g = np.load(os.path.join(GOLDEN, "pupil_ibl.npz"))
+    stack = g["stack"]
+    dfs = [pd.DataFrame(stack[e], columns=list(PUPIL_KEYS)) for e in range(len(stack))]
+    kps = [str(k) for k in g["keypoint_names"]]
+    res = ensemble_kalman_smoother_pupil(dfs, kps, "ensemble-kalman_tracker", g["A"])
+    mk = res["markers_df"].to_numpy()
+    lat = res["latents_df"].to_numpy()
+    assert np.nanmax(np.abs(mk - g["golden_markers"])) < OUT_TOL
+    assert np.abs(lat - g["golden_latents"]).max() < OUT_TOL
+    assert list(res["markers_df"].columns.get_level_values(1)[::3]) == kps
+
+
+def test_singleview_entry_point(torch):
+    from eks_amd.singleview_smoother import ensemble_kalman_smoother_single_view
+    g = np.load(os.path.join(GOLDEN, "singleview_c1.npz"))
+    obs = g["obs"]
+    dfs = [pd.DataFrame(obs[e], columns=["nose_x", "nose_y"]) for e in range(len(obs))]
+    res = ensemble_kalman_smoother_single_view(dfs, "nose", float(g["s"]), float(g["q"]))
+    out = res["markers_df"].to_numpy()[:, :2]
+    assert np.abs(out - g["out"]).max() < OUT_TOL
+    assert np.isfinite(res["nll"])
