@@ -14,7 +14,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libeks_hip.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "eks_hip.h")
 
-EKS_OK, EKS_ERR_ARG, EKS_ERR_UNSUPPORTED, EKS_SINGULAR, EKS_ERR_HIP = 0, 1, 2, 3, 4
+EKS_OK, EKS_ERR_ARG, EKS_ERR_UNSUPPORTED, EKS_ERR_HIP = 0, 1, 2, 4
+EKS_STATUS_SINGULAR, EKS_STATUS_BAD_MODEL, EKS_STATUS_SCAN = 1, 2, 4
+EKS_MODEL_A_IDENTITY, EKS_MODEL_C_IDENTITY = 1, 2
 EKS_F32, EKS_F64 = 0, 1
 EKS_MEDIAN, EKS_MEAN = 0, 1
 
@@ -37,9 +39,10 @@ SIGNATURES = {
     "eks_backward": (_i32, [_i64, _i64, _i32, _p, _p, _p, _p, _i32, _p, _p, _p, _p, _p]),
     "eks_kalman_dot": (_i32, [_i32, _i32, _i32, _p, _p, _p, _p, _p, _p, _p]),
     "eks_param_len": (_i64, [_i32, _i32]),
-    "eks_smooth_workspace_bytes": (_sz, [_i64, _i64, _i32, _i32, _i32]),
+    "eks_smooth_workspace_bytes": (_sz, [_i64, _i64, _i32, _i32, _i32, _i32]),
     "eks_smooth": (_i32, [_p, _i32, _i64, _i64, _i32, _i32, _i32, _i64, _i64, _i64, _i64, _i32,
-                          _p, _p, _i64, _i64, _i64, _p, _p, _p, _sz, _i32, _p, _p]),
+                          _p, _p, _i64, _i64, _i64, _p, _p, _p, _sz, _i32, _i32, _p, _p]),
+    "eks_smooth_chunk_len": (_i64, [_i64, _i64, _i32]),
 }
 
 _lib = None

@@ -25,7 +25,7 @@ def param_len(n: int, r: int) -> int:
     return r + 3 * r * r + n * r + n
 
 
-def pack_params(m0, S0, A, Q, C, offset, device="cuda"):
+def pack_params(m0, S0, A, Q, C, offset, device="cuda"):  # noqa: C901
     """Pack per-trajectory models into the (B, P) layout of eks_param_len:
     [m0 (r) | S0 (r*r) | A (r*r) | Q (r*r) | C (n*r) | offset (n)].
     Inputs are arrays/tensors with a leading B axis (or none, = shared)."""
@@ -62,14 +62,32 @@ def workspace(nbytes: int, device=None):
     return buf
 
 
+def model_flags(A, C) -> int:
+    """EKS_MODEL_* promise bits for host-side model arrays (A (.., r, r),
+    C (.., n, r)): set when every trajectory's A (resp. C) is the identity."""
+    A = np.asarray(A)
+    C = np.asarray(C)
+    f = 0
+    if A.shape[-1] == A.shape[-2] and np.all(A == np.eye(A.shape[-1])):
+        f |= _lib.EKS_MODEL_A_IDENTITY
+    if C.shape[-1] == C.shape[-2] and np.all(C == np.eye(C.shape[-1])):
+        f |= _lib.EKS_MODEL_C_IDENTITY
+    return f
+
+
 def smooth(obs, params, *, n: int, r: int, mode: str = "median", out=None, want_ms=False,
-           want_nll=False, status=None, algo: int = 0, stream=None):
+           want_nll=False, status=None, algo: int = 0, flags: int = 0, stream=None,
+           check: bool = False):
     """Fused ensemble -> forward -> backward -> projection for B trajectories.
 
     Returns dict(out=(B,T,n) view, ms=(B,T,r) or None, nll=(B,) or None,
-    status=(B,) int32).  ``out`` (if given) must be a (B, T, n) float64 CUDA
-    tensor/view; by default a time-major buffer is allocated so that the
-    kernel's stores are coalesced.
+    status=(B,) int32 bit mask).  ``out`` (if given) must be a (B, T, n)
+    float64 CUDA tensor/view; by default a time-major buffer is allocated so
+    that the kernel's stores are coalesced.  ``flags`` are EKS_MODEL_* promises
+    (see ``model_flags``); ``algo`` 0 = automatic, 1 = sequential, 2 =
+    time-parallel.  With ``check=True`` the call synchronises, raises on
+    singular / mis-flagged trajectories and transparently re-runs with the
+    sequential algorithm if the time-parallel scan reported a breakdown.
     """
     torch = _lib.require_gpu()
     if obs.dim() != 4:
@@ -96,7 +114,7 @@ def smooth(obs, params, *, n: int, r: int, mode: str = "median", out=None, want_
     if status is None:
         status = torch.empty((B,), dtype=torch.int32, device=dev)
     lib = _lib.load()
-    nbytes = lib.eks_smooth_workspace_bytes(B, T, n, r, algo)
+    nbytes = lib.eks_smooth_workspace_bytes(B, T, n, r, E, algo)
     ws = workspace(nbytes, dev)
     sb, st, se, sj = obs.stride()
     ob, ot, oj = out.stride()
@@ -104,9 +122,29 @@ def smooth(obs, params, *, n: int, r: int, mode: str = "median", out=None, want_
         obs.data_ptr(), dt, B, T, E, n, r, sb, st, se, sj,
         _lib.EKS_MEDIAN if mode == "median" else _lib.EKS_MEAN, params.data_ptr(),
         out.data_ptr(), ob, ot, oj, ms.data_ptr() if ms is not None else None,
-        nll.data_ptr() if nll is not None else None, ws.data_ptr(), ws.numel(), algo,
+        nll.data_ptr() if nll is not None else None, ws.data_ptr(), ws.numel(), flags, algo,
         status.data_ptr(), _lib.stream_ptr(stream)), "eks_smooth")
-    return dict(out=out, ms=ms, nll=nll, status=status)
+    res = dict(out=out, ms=ms, nll=nll, status=status)
+    if check:
+        st_all = status_bits(status)
+        if st_all & _lib.EKS_STATUS_BAD_MODEL:
+            raise ValueError("model_flags promise A = I / C = I does not hold")
+        if st_all & _lib.EKS_STATUS_SCAN and algo != 1:
+            return smooth(obs, params, n=n, r=r, mode=mode, out=out, want_ms=want_ms,
+                          want_nll=want_nll, status=status, algo=1, flags=flags,
+                          stream=stream, check=True)
+        if st_all & _lib.EKS_STATUS_SINGULAR:
+            raise np.linalg.LinAlgError("Singular matrix")
+    return res
+
+
+def status_bits(status) -> int:
+    """OR of all per-trajectory status words (synchronises)."""
+    v = 0
+    for bit in (_lib.EKS_STATUS_SINGULAR, _lib.EKS_STATUS_BAD_MODEL, _lib.EKS_STATUS_SCAN):
+        if bool(((status & bit) != 0).any().item()):
+            v |= bit
+    return v
 
 
 def make_time_major(stack_np, device="cuda", dtype=None):

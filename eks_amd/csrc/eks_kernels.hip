@@ -195,7 +195,7 @@ __global__ __launch_bounds__(64) void k_forward_dense(
     store_mat<R, R>(Sb + (TT - 1) * R * R, z);  // never written by the reference
   }
   if (nll) nll[b] = 0.5 * ((double)TT * N * kLog2Pi + log(det_m) + det_e * kLn2 + quad);
-  if (status) status[b] = ok ? 0 : EKS_SINGULAR;
+  if (status) status[b] = ok ? 0 : EKS_STATUS_SINGULAR;
 }
 
 // ------------------------------------------------------------------------
@@ -278,7 +278,7 @@ __global__ __launch_bounds__(64) void k_backward(long long B, long long TT,
 #pragma unroll
     for (int i = 0; i < R; ++i) msn[i] = msc[i];
   }
-  if (status) status[b] = ok ? 0 : EKS_SINGULAR;
+  if (status) status[b] = ok ? 0 : EKS_STATUS_SINGULAR;
 }
 
 // ------------------------------------------------------------------------
@@ -325,7 +325,7 @@ __global__ void k_kalman_dot(int k, const double *x, const double *Vg, const dou
       out[i * k + c] = s;
     }
   }
-  if (status) status[0] = ok ? 0 : EKS_SINGULAR;
+  if (status) status[0] = ok ? 0 : EKS_STATUS_SINGULAR;
 }
 
 }  // namespace eks

@@ -1,0 +1,13 @@
+// Fused-smoother kernels instantiated for latent r = 3, observations n = 6
+// (one translation unit per shape so hipcc compiles them in parallel).
+#include "smooth_impl.hpp"
+
+namespace eks {
+
+int launch_36(const SmoothArgs &a, int algo, long long L) {
+  const int flags = a.flags;
+  if (flags & EKS_MODEL_A_IDENTITY) return launch_shape<3, 6, true, false>(a, algo, L);
+  return launch_shape<3, 6, false, false>(a, algo, L);
+}
+
+}  // namespace eks

@@ -1,0 +1,77 @@
+// C ABI of the fused smoother: eks_smooth, eks_smooth_workspace_bytes,
+// eks_smooth_chunk_len (include/eks_hip.h).  Validates arguments, zeroes the
+// status array, picks the algorithm and dispatches to the per-shape
+// launchers of eks_shape_*.hip.
+#include "smooth_impl.hpp"
+
+using namespace eks;
+
+namespace {
+
+// automatic choice: the time-parallel scan whenever it creates more than one
+// chunk per trajectory (i.e. B alone does not fill the GPU), else sequential
+// (and a requested time-parallel run with a single chunk runs sequentially)
+int pick_algo(long long B, long long T, int r, int algo) {
+  const long long L = chunk_len(B, T, r);
+  if (algo == 1) return 1;
+  return L >= T ? 1 : 2;
+}
+
+bool shape_supported(int r, int n) {
+  return (r == 2 && n == 2) || (r == 3 && (n == 4 || n == 6 || n == 8));
+}
+
+}  // namespace
+
+extern "C" {
+
+int64_t eks_smooth_chunk_len(int64_t B, int64_t T, int r) {
+  if (B <= 0 || T <= 0 || r < 1) return 0;
+  const long long L = chunk_len(B, T, r);
+  return L >= T ? 0 : L;
+}
+
+size_t eks_smooth_workspace_bytes(int64_t B, int64_t T, int n, int r, int E, int algo) {
+  (void)E;
+  if (B <= 0 || T <= 0 || r < 1 || n < 1) return 0;
+  const int al = pick_algo(B, T, r, algo);
+  if (al == 1) return seq_workspace_bytes(B, T, r);
+  return make_plan(B, T, r, n, chunk_len(B, T, r)).total;
+}
+
+int eks_smooth(const void *obs, int obs_dtype, int64_t B, int64_t T, int E, int n, int r,
+               int64_t sb, int64_t st, int64_t se, int64_t sj, int mode, const double *params,
+               double *out, int64_t ob, int64_t ot, int64_t oj, double *ms, double *nll,
+               void *workspace, size_t workspace_bytes, int model_flags, int algo,
+               int32_t *status, void *stream) {
+  if (!obs || !params || !out || !status) return set_err(EKS_ERR_ARG, "eks_smooth: NULL pointer");
+  if (B < 0 || T < 1 || E < 1) return set_err(EKS_ERR_ARG, "eks_smooth: need B>=0, T>=1, E>=1");
+  if (E > kMaxMembers) return set_err(EKS_ERR_UNSUPPORTED, "eks_smooth: E=%d > %d", E, kMaxMembers);
+  if (mode != EKS_MEDIAN && mode != EKS_MEAN)
+    return set_err(EKS_ERR_ARG, "%d averaging not supported", mode);
+  if (obs_dtype != EKS_F32 && obs_dtype != EKS_F64) return set_err(EKS_ERR_ARG, "bad dtype");
+  if (algo < 0 || algo > 2) return set_err(EKS_ERR_ARG, "eks_smooth: algo %d unknown", algo);
+  if (!shape_supported(r, n))
+    return set_err(EKS_ERR_UNSUPPORTED,
+                   "eks_smooth: (r=%d, n=%d) not compiled in (have (2,2) (3,4) (3,6) (3,8))", r, n);
+  if ((model_flags & EKS_MODEL_C_IDENTITY) && r != n)
+    return set_err(EKS_ERR_ARG, "eks_smooth: C = I needs r == n");
+  if (B == 0) return EKS_OK;
+  const int al = pick_algo(B, T, r, algo);
+  const size_t need = eks_smooth_workspace_bytes(B, T, n, r, E, al);
+  if (!workspace || workspace_bytes < need)
+    return set_err(EKS_ERR_ARG, "eks_smooth: workspace of %zu bytes needed", need);
+  hipStream_t s = (hipStream_t)stream;
+  if (hipMemsetAsync(status, 0, (size_t)B * sizeof(int32_t), s) != hipSuccess)
+    return set_err(EKS_ERR_HIP, "eks_smooth: hipMemsetAsync(status) failed");
+  SmoothArgs a{obs,    obs_dtype, B,  T,  E,         n,     r,  sb,      st,    se,
+               sj,     mode == EKS_MEDIAN ? 1 : 0,  params, out, ob, ot, oj, ms,    nll,
+               (char *)workspace, workspace_bytes, model_flags, al, status, s};
+  const long long L = chunk_len(B, T, r);
+  if (r == 2 && n == 2) return launch_22(a, al, L);
+  if (n == 4) return launch_34(a, al, L);
+  if (n == 6) return launch_36(a, al, L);
+  return launch_38(a, al, L);
+}
+
+}  // extern "C"

@@ -1,0 +1,573 @@
+// Per-timestep building blocks of the EKS recursions, shared by the
+// sequential (eks_smooth.hip) and time-parallel (eks_chunked.hip) kernels.
+//
+// Conventions: R = latent dimension r, N = observation dimension n.
+// AI = "A is the identity" and CI = "C is the identity (R == N)" are
+// compile-time structure flags: the single-view model has A = C = I2
+//  and the multi-camera model A = I3
+// (eks/multiview_pca_smoother.py:724).  The host promises the structure and
+// the kernels verify it per trajectory (status bit EKS_STATUS_BAD_MODEL on violation).
+#pragma once
+#include "eks_common.hpp"
+#include "small_linalg.hpp"
+
+namespace eks {
+
+template <int R>
+struct Sym {
+  static constexpr int len = R * (R + 1) / 2;
+  static constexpr int idx(int i, int j) {
+    return i <= j ? i * R - i * (i - 1) / 2 + (j - i) : j * R - j * (j - 1) / 2 + (i - j);
+  }
+};
+
+// 1/x to ~1 ulp: hardware reciprocal + two Newton-Raphson steps (5 VALU ops
+// instead of the ~10 of an IEEE division).
+EKS_DEV double rcp_nr(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  double e = fma(-x, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-x, r, 1.0);
+  return fma(r, e, r);
+}
+
+// x / d correctly rounded (== IEEE division, as numpy's true_divide) for a
+// small integer d, by one fma correction of x * RN(1/d) (Markstein); checked
+// exhaustively against true division on random doubles for d in 3..10.
+EKS_DEV double div_small_int(double x, double d, double inv_d) {
+  const double q = x * inv_d;
+  const double r = fma(-q, d, x);
+  return fma(r, inv_d, q);
+}
+
+template <int R>
+EKS_DEV bool is_identity(const double (&M)[R][R]) {
+  bool ok = true;
+#pragma unroll
+  for (int i = 0; i < R; ++i)
+#pragma unroll
+    for (int j = 0; j < R; ++j) ok = ok && (M[i][j] == (i == j ? 1.0 : 0.0));
+  return ok;
+}
+
+template <int N, int R>
+EKS_DEV bool is_identity_rect(const double (&M)[N][R]) {
+  bool ok = (N == R);
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+#pragma unroll
+    for (int j = 0; j < R; ++j) ok = ok && (M[i][j] == (i == j ? 1.0 : 0.0));
+  return ok;
+}
+
+// ---------------------------------------------------------------------------
+// Ensemble reduction of one step (E members x N coordinates in registers).
+// Same arithmetic as ensemble_reduce (numpy order, exact divisions).
+// ---------------------------------------------------------------------------
+template <int E, typename T>
+EKS_DEV void median_of(const T (&raw)[E], double &med) {
+  T s[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) s[e] = raw[e];
+  if constexpr (E == 3) {
+    const T lo = fmin(s[0], s[1]), hi = fmax(s[0], s[1]);
+    med = (double)fmax(lo, fmin(hi, s[2]));
+  } else if constexpr (E == 5) {
+    // median of 5: drop the min and max of {s0..s3} (never the median of 5),
+    // then the median of the two survivors and s4
+    T a = fmin(s[0], s[1]), b = fmax(s[0], s[1]);
+    T c = fmin(s[2], s[3]), d = fmax(s[2], s[3]);
+    T lo = fmax(a, c);          // second smallest candidate
+    T hi = fmin(b, d);          // second largest candidate
+    T x = s[4];
+    T l2 = fmin(lo, hi), h2 = fmax(lo, hi);
+    med = (double)fmax(l2, fmin(h2, x));
+  } else {
+#pragma unroll
+    for (int p = 0; p < E; ++p)
+#pragma unroll
+      for (int i = p & 1; i + 1 < E; i += 2) {
+        const T a = s[i], b = s[i + 1];
+        s[i] = a < b ? a : b;
+        s[i + 1] = a < b ? b : a;
+      }
+    if constexpr (E % 2 == 1)
+      med = (double)s[E / 2];
+    else
+      med = ((double)s[E / 2 - 1] + (double)s[E / 2]) * 0.5;
+  }
+}
+
+template <int E, typename T>
+EKS_DEV void ensemble_col(const T (&raw)[E], bool median, double &avg, double &var) {
+  constexpr double dE = (double)E;
+  constexpr double invE = 1.0 / (double)E;
+  double x[E];
+  bool nan = false;
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    x[e] = (double)raw[e];
+    nan |= (x[e] != x[e]);
+  }
+  double s;
+  if constexpr (E < 8) {
+    s = x[0];
+#pragma unroll
+    for (int e = 1; e < E; ++e) s += x[e];
+  } else {
+    s = np_sum<E>(x);
+  }
+  const double mean = div_small_int(s, dE, invE);
+  double d[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const double t = x[e] - mean;
+    d[e] = t * t;
+  }
+  double ss;
+  if constexpr (E < 8) {
+    ss = d[0];
+#pragma unroll
+    for (int e = 1; e < E; ++e) ss += d[e];
+  } else {
+    ss = np_sum<E>(d);
+  }
+  var = div_small_int(div_small_int(ss, dE, invE), dE, invE);
+  if (median)
+    median_of<E, T>(raw, avg);
+  else
+    avg = mean;
+  if (nan) {
+    avg = __builtin_nan("");
+    var = __builtin_nan("");
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Kalman filter pieces
+// ---------------------------------------------------------------------------
+// prior of step t from the posterior of t-1:  m <- A m,  P <- A (P A^T) + Q
+template <int R, bool AI>
+EKS_DEV void kf_predict(double (&m)[R], double (&P)[R][R], const double (&A)[R][R],
+                        const double (&Q)[R][R]) {
+  if constexpr (AI) {
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+#pragma unroll
+      for (int j = i; j < R; ++j) {
+        P[i][j] += Q[i][j];
+        if (j != i) P[j][i] = P[i][j];
+      }
+  } else {
+    double PAt[R][R], mp[R];
+    matmul_nt<R, R, R>(P, A, PAt);
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+#pragma unroll
+      for (int j = i; j < R; ++j) {
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < R; ++k) s = fma(A[i][k], PAt[k][j], s);
+        P[i][j] = s + Q[i][j];
+      }
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+#pragma unroll
+      for (int j = 0; j < i; ++j) P[i][j] = P[j][i];
+    matvec<R, R>(A, m, mp);
+#pragma unroll
+    for (int i = 0; i < R; ++i) m[i] = mp[i];
+  }
+}
+
+// NLL accumulator: quad = sum e^2/s, log det = log(mant) + ex ln 2
+struct NllAcc {
+  double quad = 0.0, mant = 1.0;
+  int ex = 0;
+  EKS_DEV void add(double e, double s, double inv) {
+    quad = fma(e * e, inv, quad);
+    mant *= s;
+  }
+  EKS_DEV void renorm() {
+    int k;
+    mant = frexp(mant, &k);
+    ex += k;
+  }
+  EKS_DEV double value(double n_terms) const {
+    return 0.5 * (n_terms * kLog2Pi + log(mant) + ex * kLn2 + quad);
+  }
+};
+
+// Measurement update with diagonal R, one scalar observation at a time
+// (algebraically the reference's kalman_dot with the n x n solve).
+template <int R, int N, bool CI>
+EKS_DEV void kf_update(double (&m)[R], double (&P)[R][R], const double (&C)[N][R],
+                       const double (&y)[N], const double (&rv)[N], NllAcc &acc, bool &ok) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    double v[R], s, hm;
+    if constexpr (CI) {
+#pragma unroll
+      for (int a = 0; a < R; ++a) v[a] = P[a][i];
+      s = v[i] + rv[i];
+      hm = m[i];
+    } else {
+#pragma unroll
+      for (int a = 0; a < R; ++a) {
+        double t = 0.0;
+#pragma unroll
+        for (int k = 0; k < R; ++k) t = fma(P[a][k], C[i][k], t);
+        v[a] = t;
+      }
+      s = rv[i];
+      hm = 0.0;
+#pragma unroll
+      for (int k = 0; k < R; ++k) {
+        s = fma(C[i][k], v[k], s);
+        hm = fma(C[i][k], m[k], hm);
+      }
+    }
+    ok = ok && !(s <= 0.0);  // NaN propagates as in numpy, not an error
+    const double inv = rcp_nr(s);
+    const double e = y[i] - hm;
+    acc.add(e, s, inv);
+    const double ei = e * inv;
+#pragma unroll
+    for (int a = 0; a < R; ++a) m[a] = fma(v[a], ei, m[a]);
+#pragma unroll
+    for (int a = 0; a < R; ++a) {
+      const double ka = v[a] * inv;
+#pragma unroll
+      for (int c = a; c < R; ++c) {
+        P[a][c] = fma(-ka, v[c], P[a][c]);
+        if (c != a) P[c][a] = P[a][c];
+      }
+    }
+  }
+  acc.renorm();
+}
+
+// Inverse of a symmetric positive definite R x R matrix (closed form for
+// R <= 2, Gauss-Jordan with partial pivoting above).  false if singular.
+template <int R>
+EKS_DEV bool spd_inverse(const double (&S)[R][R], double (&Si)[R][R]) {
+  if constexpr (R == 1) {
+    Si[0][0] = rcp_nr(S[0][0]);
+    return S[0][0] != 0.0;
+  } else if constexpr (R == 2) {
+    const double det = fma(S[0][0], S[1][1], -S[0][1] * S[1][0]);
+    const double id = rcp_nr(det);
+    Si[0][0] = S[1][1] * id;
+    Si[1][1] = S[0][0] * id;
+    Si[0][1] = -S[0][1] * id;
+    Si[1][0] = -S[1][0] * id;
+    return det != 0.0;
+  } else if constexpr (R == 3) {
+    const double c00 = fma(S[1][1], S[2][2], -S[1][2] * S[2][1]);
+    const double c01 = fma(S[1][2], S[2][0], -S[1][0] * S[2][2]);
+    const double c02 = fma(S[1][0], S[2][1], -S[1][1] * S[2][0]);
+    const double det = fma(S[0][0], c00, fma(S[0][1], c01, S[0][2] * c02));
+    const double id = rcp_nr(det);
+    Si[0][0] = c00 * id;
+    Si[1][0] = c01 * id;
+    Si[2][0] = c02 * id;
+    Si[0][1] = fma(S[0][2], S[2][1], -S[0][1] * S[2][2]) * id;
+    Si[1][1] = fma(S[0][0], S[2][2], -S[0][2] * S[2][0]) * id;
+    Si[2][1] = fma(S[0][1], S[2][0], -S[0][0] * S[2][1]) * id;
+    Si[0][2] = fma(S[0][1], S[1][2], -S[0][2] * S[1][1]) * id;
+    Si[1][2] = fma(S[0][2], S[1][0], -S[0][0] * S[1][2]) * id;
+    Si[2][2] = fma(S[0][0], S[1][1], -S[0][1] * S[1][0]) * id;
+    return det != 0.0;
+  } else {
+    double a[R][R];
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+#pragma unroll
+      for (int j = 0; j < R; ++j) {
+        a[i][j] = S[i][j];
+        Si[i][j] = (i == j) ? 1.0 : 0.0;
+      }
+    return gauss_solve<R, R>(a, Si);
+  }
+}
+
+// RTS gain and offset at step t from the filtered (m, P):
+//   S = A P A^T + Q,  J = P A^T S^-1,  d = m - J A m
+// so that ms[t] = J ms[t+1] + d  (eks/ensemble_kalman.py:158, :161).
+template <int R, bool AI>
+EKS_DEV bool rts_gain(const double (&m)[R], const double (&P)[R][R], const double (&A)[R][R],
+                      const double (&Q)[R][R], double (&J)[R][R], double (&d)[R]) {
+  double S[R][R], PAt[R][R], Si[R][R];
+  if constexpr (AI) {
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+#pragma unroll
+      for (int j = 0; j < R; ++j) {
+        S[i][j] = P[i][j] + Q[i][j];
+        PAt[i][j] = P[i][j];
+      }
+  } else {
+    matmul_nt<R, R, R>(P, A, PAt);
+    matmul<R, R, R>(A, PAt, S);
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+#pragma unroll
+      for (int j = 0; j < R; ++j) S[i][j] += Q[i][j];
+  }
+  const bool ok = spd_inverse<R>(S, Si);
+  matmul<R, R, R>(PAt, Si, J);
+  double Am[R];
+  if constexpr (AI) {
+#pragma unroll
+    for (int i = 0; i < R; ++i) Am[i] = m[i];
+  } else {
+    matvec<R, R>(A, m, Am);
+  }
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    double s = m[i];
+#pragma unroll
+    for (int k = 0; k < R; ++k) s = fma(-J[i][k], Am[k], s);
+    d[i] = s;
+  }
+  return ok;
+}
+
+template <int R, int N, bool CI>
+EKS_DEV void project_store(double *out, long long oj, const double (&C)[N][R],
+                           const double (&ms)[R], const double (&off)[N]) {
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    double cm;
+    if constexpr (CI) {
+      cm = ms[j];
+    } else {
+      cm = 0.0;
+#pragma unroll
+      for (int k = 0; k < R; ++k) cm = fma(C[j][k], ms[k], cm);
+    }
+    out[j * oj] = cm + off[j];
+  }
+}
+
+}  // namespace eks
+
+namespace eks {
+
+// ---------------------------------------------------------------------------
+// Time-parallel (associative) filtering elements, Sarkka & Garcia-Fernandez,
+// "Temporal parallelization of Bayesian smoothers" (IEEE TAC 2021).  An
+// element summarises a chunk of steps [s, e) as a function of the unknown
+// state x_{s-1}:
+//     p(x_{e-1} | x_{s-1}, y_{s..e-1}) = N(Ab x_{s-1} + bb, Cb)
+//     p(y_{s..e-1} | x_{s-1})          ~ exp(-1/2 x^T Jb x + eta^T x)
+// It is built here one step and one scalar observation at a time (R_t is
+// diagonal), so no matrix inverse is needed inside a chunk.
+// ---------------------------------------------------------------------------
+template <int R>
+struct Elem {
+  double Ab[R][R], bb[R], Cb[R][R], eta[R], Jb[R][R];
+  static constexpr int len = R * R + R + Sym<R>::len + R + Sym<R>::len;
+
+  EKS_DEV void set_identity() {
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      bb[i] = 0.0;
+      eta[i] = 0.0;
+#pragma unroll
+      for (int j = 0; j < R; ++j) {
+        Ab[i][j] = (i == j) ? 1.0 : 0.0;
+        Cb[i][j] = 0.0;
+        Jb[i][j] = 0.0;
+      }
+    }
+  }
+  // strided store / load: component k at p[k * stride]
+  EKS_DEV void store(double *p, long long stride) const {
+    int k = 0;
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+#pragma unroll
+      for (int j = 0; j < R; ++j) p[(k++) * stride] = Ab[i][j];
+#pragma unroll
+    for (int i = 0; i < R; ++i) p[(k++) * stride] = bb[i];
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+#pragma unroll
+      for (int j = i; j < R; ++j) p[(k++) * stride] = Cb[i][j];
+#pragma unroll
+    for (int i = 0; i < R; ++i) p[(k++) * stride] = eta[i];
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+#pragma unroll
+      for (int j = i; j < R; ++j) p[(k++) * stride] = Jb[i][j];
+  }
+  EKS_DEV void load(const double *p, long long stride) {
+    int k = 0;
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+#pragma unroll
+      for (int j = 0; j < R; ++j) Ab[i][j] = p[(k++) * stride];
+#pragma unroll
+    for (int i = 0; i < R; ++i) bb[i] = p[(k++) * stride];
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+#pragma unroll
+      for (int j = i; j < R; ++j) Cb[i][j] = Cb[j][i] = p[(k++) * stride];
+#pragma unroll
+    for (int i = 0; i < R; ++i) eta[i] = p[(k++) * stride];
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+#pragma unroll
+      for (int j = i; j < R; ++j) Jb[i][j] = Jb[j][i] = p[(k++) * stride];
+  }
+};
+
+// Absorb one time step (predict with A, Q; update with the N scalar
+// observations of y, rv) into the running element.
+template <int R, int N, bool AI, bool CI>
+EKS_DEV void elem_absorb(Elem<R> &E, const double (&A)[R][R], const double (&Q)[R][R],
+                         const double (&C)[N][R], const double (&y)[N], const double (&rv)[N],
+                         bool &ok) {
+  if constexpr (AI) {
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+#pragma unroll
+      for (int j = i; j < R; ++j) {
+        E.Cb[i][j] += Q[i][j];
+        if (j != i) E.Cb[j][i] = E.Cb[i][j];
+      }
+  } else {
+    double T1[R][R], T2[R][R], b2[R];
+    matmul<R, R, R>(A, E.Ab, T1);
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+#pragma unroll
+      for (int j = 0; j < R; ++j) E.Ab[i][j] = T1[i][j];
+    matvec<R, R>(A, E.bb, b2);
+#pragma unroll
+    for (int i = 0; i < R; ++i) E.bb[i] = b2[i];
+    matmul_nt<R, R, R>(E.Cb, A, T2);
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+#pragma unroll
+      for (int j = i; j < R; ++j) {
+        double s = Q[i][j];
+#pragma unroll
+        for (int k = 0; k < R; ++k) s = fma(A[i][k], T2[k][j], s);
+        E.Cb[i][j] = s;
+      }
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+#pragma unroll
+      for (int j = 0; j < i; ++j) E.Cb[i][j] = E.Cb[j][i];
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    double v[R], g[R], s, hb;
+    if constexpr (CI) {
+#pragma unroll
+      for (int a = 0; a < R; ++a) {
+        v[a] = E.Cb[a][i];
+        g[a] = E.Ab[i][a];
+      }
+      s = v[i] + rv[i];
+      hb = E.bb[i];
+    } else {
+#pragma unroll
+      for (int a = 0; a < R; ++a) {
+        double tv = 0.0, tg = 0.0;
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+          tv = fma(E.Cb[a][k], C[i][k], tv);
+          tg = fma(E.Ab[k][a], C[i][k], tg);
+        }
+        v[a] = tv;
+        g[a] = tg;
+      }
+      s = rv[i];
+      hb = 0.0;
+#pragma unroll
+      for (int k = 0; k < R; ++k) {
+        s = fma(C[i][k], v[k], s);
+        hb = fma(C[i][k], E.bb[k], hb);
+      }
+    }
+    ok = ok && !(s <= 0.0);
+    const double inv = rcp_nr(s);
+    const double e0 = y[i] - hb;
+    const double ei = e0 * inv;
+#pragma unroll
+    for (int a = 0; a < R; ++a) {
+      const double ga = g[a] * inv;
+      E.eta[a] = fma(g[a], ei, E.eta[a]);
+#pragma unroll
+      for (int c = a; c < R; ++c) {
+        E.Jb[a][c] = fma(ga, g[c], E.Jb[a][c]);
+        if (c != a) E.Jb[c][a] = E.Jb[a][c];
+      }
+    }
+#pragma unroll
+    for (int a = 0; a < R; ++a) {
+      const double ka = v[a] * inv;
+      E.bb[a] = fma(ka, e0, E.bb[a]);
+#pragma unroll
+      for (int c = 0; c < R; ++c) E.Ab[a][c] = fma(-ka, g[c], E.Ab[a][c]);
+#pragma unroll
+      for (int c = a; c < R; ++c) {
+        E.Cb[a][c] = fma(-ka, v[c], E.Cb[a][c]);
+        if (c != a) E.Cb[c][a] = E.Cb[a][c];
+      }
+    }
+  }
+}
+
+// Filtered state (m, P) at step s-1 combined with the element of [s, e):
+//   P' = Ab (I + P Jb)^-1 P Ab^T + Cb,   m' = Ab (I + P Jb)^-1 (m + P eta) + bb
+template <int R>
+EKS_DEV bool compose_state(double (&m)[R], double (&P)[R][R], const Elem<R> &E) {
+  double M[R][R], X[R][1 + R];
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    double pe = m[i];
+#pragma unroll
+    for (int k = 0; k < R; ++k) pe = fma(P[i][k], E.eta[k], pe);
+    X[i][0] = pe;
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      double t = (i == j) ? 1.0 : 0.0, u = 0.0;
+#pragma unroll
+      for (int k = 0; k < R; ++k) {
+        t = fma(P[i][k], E.Jb[k][j], t);
+        u = fma(P[i][k], E.Ab[j][k], u);
+      }
+      M[i][j] = t;
+      X[i][1 + j] = u;
+    }
+  }
+  const bool ok = gauss_solve<R, 1 + R>(M, X);
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    double s = E.bb[i];
+#pragma unroll
+    for (int k = 0; k < R; ++k) s = fma(E.Ab[i][k], X[k][0], s);
+    m[i] = s;
+  }
+  double Pn[R][R];
+#pragma unroll
+  for (int i = 0; i < R; ++i)
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      double s = E.Cb[i][j];
+#pragma unroll
+      for (int k = 0; k < R; ++k) s = fma(E.Ab[i][k], X[k][1 + j], s);
+      Pn[i][j] = s;
+    }
+#pragma unroll
+  for (int i = 0; i < R; ++i)
+#pragma unroll
+    for (int j = 0; j < R; ++j) P[i][j] = 0.5 * (Pn[i][j] + Pn[j][i]);
+  return ok;
+}
+
+}  // namespace eks

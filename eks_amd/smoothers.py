@@ -28,9 +28,8 @@ def _run_fused(stack: np.ndarray, model: dict, mode: str = "median", want_ms=Fal
     obs = obs.permute(1, 0, 2).unsqueeze(0)  # (1, T, E, n) view, no copy
     params = batch.pack_params(model["m0"], model["S0"], model["A"], model["Q"], model["C"],
                                model["offset"])
-    res = batch.smooth(obs, params, n=n, r=r, mode=mode, want_ms=want_ms, want_nll=want_nll)
-    if bool((res["status"] != 0).any().item()):
-        raise np.linalg.LinAlgError("Singular matrix")
+    res = batch.smooth(obs, params, n=n, r=r, mode=mode, want_ms=want_ms, want_nll=want_nll,
+                       flags=batch.model_flags(model["A"], model["C"]), check=True)
     out = res["out"][0].cpu().numpy()
     ms = res["ms"][0].cpu().numpy() if want_ms else None
     nll = float(res["nll"][0].item()) if want_nll else None

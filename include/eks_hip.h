@@ -20,9 +20,16 @@
  *     index b in [0, B); a "trajectory" is one (video, keypoint) series.
  *   - Return value: EKS_OK or an error code; eks_last_error() gives the text
  *     (thread-local).  Numerical failures are reported per trajectory in the
- *     optional int32 `status` array (device, length B):
- *       0 = ok, EKS_SINGULAR = a matrix the reference would hand to
- *       np.linalg.solve was singular (the reference raises LinAlgError).
+ *     optional int32 `status` array (device, length B), a bit mask:
+ *       0 = ok
+ *       EKS_STATUS_SINGULAR   a matrix the reference would hand to
+ *                             np.linalg.solve was singular (the reference
+ *                             raises LinAlgError there)
+ *       EKS_STATUS_BAD_MODEL  a model_flags promise (A or C = identity) does
+ *                             not hold for this trajectory's parameters
+ *       EKS_STATUS_SCAN       the time-parallel scan could not form a chunk
+ *                             summary (singular Q with exact observations);
+ *                             rerun that batch with algo = 1
  *     NaNs propagate exactly as in numpy and are not an error.
  */
 #ifndef EKS_HIP_H
@@ -39,9 +46,14 @@ enum {
   EKS_OK = 0,
   EKS_ERR_ARG = 1,         /* bad size / NULL pointer / bad mode */
   EKS_ERR_UNSUPPORTED = 2, /* (r, n, E) combination not compiled in */
-  EKS_ERR_HIP = 4,         /* a HIP runtime call failed */
-  EKS_SINGULAR = 3         /* per-trajectory status value */
+  EKS_ERR_HIP = 4          /* a HIP runtime call failed */
 };
+
+/* per-trajectory status bits */
+enum { EKS_STATUS_SINGULAR = 1, EKS_STATUS_BAD_MODEL = 2, EKS_STATUS_SCAN = 4 };
+
+/* model structure promises for eks_smooth (verified per trajectory) */
+enum { EKS_MODEL_A_IDENTITY = 1, EKS_MODEL_C_IDENTITY = 2 };
 
 enum { EKS_F32 = 0, EKS_F64 = 1 };
 enum { EKS_MEDIAN = 0, EKS_MEAN = 1 };
@@ -139,17 +151,26 @@ int64_t eks_param_len(int n, int r);
  *   out      smoothed observations out(b,t,j) = out[b*ob + t*ot + j*oj] (f64)
  *   ms       (B, T, r) contiguous smoothed latents, or NULL
  *   nll      (B) or NULL
+ *   model_flags  EKS_MODEL_A_IDENTITY / EKS_MODEL_C_IDENTITY: the caller
+ *            promises A = I (and C = I, r = n) for every trajectory, which
+ *            selects kernels that skip those products (single-view: both;
+ *            multi-camera: A).  Violations are flagged in `status`.
  *   workspace / workspace_bytes: device scratch of at least
  *            eks_smooth_workspace_bytes(...) bytes (not zeroed by caller).
  *   algo     0 = automatic, 1 = sequential (one lane per trajectory),
  *            2 = time-parallel chunked scan
+ *   status   (B) int32, REQUIRED; zeroed by the call, then bit flags as above.
  */
-size_t eks_smooth_workspace_bytes(int64_t B, int64_t T, int n, int r, int algo);
+size_t eks_smooth_workspace_bytes(int64_t B, int64_t T, int n, int r, int E, int algo);
 int eks_smooth(const void *obs, int obs_dtype, int64_t B, int64_t T, int E, int n, int r,
                int64_t sb, int64_t st, int64_t se, int64_t sj, int mode, const double *params,
                double *out, int64_t ob, int64_t ot, int64_t oj, double *ms, double *nll,
-               void *workspace, size_t workspace_bytes, int algo, int32_t *status,
-               void *stream);
+               void *workspace, size_t workspace_bytes, int model_flags, int algo,
+               int32_t *status, void *stream);
+
+/* Chunk length the time-parallel algorithm uses for (B, T, r) (0 if algo 1
+ * would be chosen automatically).  Exposed for tests and DESIGN.md. */
+int64_t eks_smooth_chunk_len(int64_t B, int64_t T, int r);
 
 #ifdef __cplusplus
 }

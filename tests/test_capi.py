@@ -24,13 +24,18 @@ def test_limits_and_sizes():
     assert lib.eks_max_latent() >= 3 and lib.eks_max_obs() >= 8 and lib.eks_max_members() >= 8
     for n, r in [(2, 2), (8, 3), (4, 3)]:
         assert lib.eks_param_len(n, r) == r + 3 * r * r + n * r + n
-    assert lib.eks_smooth_workspace_bytes(10, 100, 2, 2, 1) >= 10 * 100 * 5 * 8
+    assert lib.eks_smooth_workspace_bytes(10, 100, 2, 2, 5, 1) >= 10 * 100 * 5 * 8
+    # time-parallel plan: few long trajectories are cut into chunks
+    L = lib.eks_smooth_chunk_len(17, 100000, 2)
+    assert 64 <= L < 100000 and L % 8 == 0
+    assert lib.eks_smooth_chunk_len(1 << 20, 1000, 2) == 0  # enough trajectories: sequential
+    assert lib.eks_smooth_workspace_bytes(17, 100000, 2, 2, 5, 2) >= 17 * 100000 * 2 * 16
 
 
 def test_argument_errors_do_not_launch():
     lib = _lib.load()
     rc = lib.eks_smooth(None, 0, 1, 10, 5, 2, 2, 0, 0, 0, 0, 0, None, None, 0, 0, 0,
-                        None, None, None, 0, 0, None, None)
+                        None, None, None, 0, 0, 0, None, None)
     assert rc == _lib.EKS_ERR_ARG
     assert b"NULL" in lib.eks_last_error()
     rc = lib.eks_ensemble(ctypes.c_void_p(8), 0, 1, 10, 5, 2, 0, 0, 0, 0, 7,

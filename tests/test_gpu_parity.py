@@ -211,9 +211,12 @@ def _oracle_smooth_batch(stacks, models, O):
     return outs
 
 
-@pytest.mark.parametrize("r,n,E", [(2, 2, 5), (3, 4, 5), (3, 6, 4), (3, 8, 5), (2, 2, 11)])
-def test_fused_batch_vs_oracle(torch, r, n, E):
-    """B independent trajectories with different models and layouts."""
+@pytest.mark.parametrize("algo", [1, 2])
+@pytest.mark.parametrize("r,n,E", [(2, 2, 5), (3, 4, 5), (3, 6, 4), (3, 8, 5), (2, 2, 11),
+                                   (2, 2, 3)])
+def test_fused_batch_vs_oracle(torch, r, n, E, algo):
+    """B independent trajectories with different models and layouts, both
+    algorithms (1 = sequential, 2 = time-parallel chunked scan)."""
     from eks_amd import batch, synthetic
     from oracle import eks_oracle as O
     rng = np.random.default_rng(100 * r + n)
@@ -239,17 +242,22 @@ def test_fused_batch_vs_oracle(torch, r, n, E):
                                np.stack([m["C"] for m in models]),
                                np.stack([m["offset"] for m in models]))
     ref = _oracle_smooth_batch(list(stacks), models, O)
+    flags = batch.model_flags(np.stack([m["A"] for m in models]),
+                              np.stack([m["C"] for m in models]))
     # time-major float32 layout (the bench layout)
     d = batch.make_time_major(stacks, dtype=np.float32)
-    res = batch.smooth(d, params, n=n, r=r, want_nll=True)
+    res = batch.smooth(d, params, n=n, r=r, want_nll=True, algo=algo, flags=flags)
     out = res["out"].cpu().numpy()
     assert (res["status"] == 0).all()
     err = max(np.abs(out[b] - ref[b]).max() for b in range(B))
     assert err < OUT_TOL, err
     # trajectory-major float64 layout gives the same numbers
     d64 = torch.from_numpy(np.ascontiguousarray(stacks.transpose(0, 2, 1, 3))).cuda()  # (B,T,E,n)
-    res2 = batch.smooth(d64, params, n=n, r=r, want_nll=True)
-    np.testing.assert_array_equal(res2["out"].cpu().numpy(), out)
+    res2 = batch.smooth(d64, params, n=n, r=r, want_nll=True, algo=algo, flags=flags)
+    np.testing.assert_allclose(res2["out"].cpu().numpy(), out, rtol=0, atol=1e-9)
+    # without structure flags (general A, C code path) the same numbers
+    res3 = batch.smooth(d, params, n=n, r=r, want_nll=True, algo=algo, flags=0)
+    np.testing.assert_allclose(res3["out"].cpu().numpy(), out, rtol=0, atol=1e-9)
     # NLL per trajectory vs the oracle's definition
     for b in (0, B // 2, B - 1):
         preds, ev = O.ensemble_array(stacks[b])
@@ -258,26 +266,92 @@ def test_fused_batch_vs_oracle(torch, r, n, E):
         assert abs(float(res["nll"][b]) - nll) <= 1e-9 * abs(nll)
 
 
+@pytest.mark.parametrize("kind", ["singleview_heavy", "pupil_like", "multiview"])
+def test_time_parallel_long_trajectories(torch, kind):
+    """Few long trajectories (the configs 2/3/5 regime): the chunked scan
+    (algo 2, hundreds of chunks per trajectory) against the sequential
+    kernel on every trajectory and against the oracle on two of them."""
+    from eks_amd import batch, synthetic
+    from oracle import eks_oracle as O
+    rng = np.random.default_rng(11)
+    B, T, E = 6, 30000, 5
+    if kind == "multiview":
+        st = synthetic.multiview_obs(rng, 4, E, T, K=B).transpose(2, 0, 1, 3).astype(np.float64)
+        r, n = 3, 8
+    elif kind == "pupil_like":
+        st = np.stack([synthetic.pupil_obs(rng, E, T, a=0.999) for _ in range(B)]).astype(np.float64)
+        r, n = 3, 8
+    else:
+        st = synthetic.singleview_obs(rng, E, T, K=B).transpose(2, 0, 1, 3).astype(np.float64)
+        r, n = 2, 2
+    models = []
+    for b in range(B):
+        preds, ev = O.ensemble_array(st[b])
+        if kind == "singleview_heavy":
+            p = O.singleview_params(preds, ev, 0.001, 25)
+            p["offset"] = p["means"]
+        elif kind == "multiview":
+            p = O.multicam_params(preds, ev, 0.01, 25)
+            p["offset"] = p["means"]
+        else:
+            p = O.pupil_params(preds, np.diag([0.9999, 0.999, 0.999]))
+            p["offset"] = p["means"]
+        models.append(p)
+    stackp = lambda k: np.stack([m[k] for m in models])  # noqa: E731
+    params = batch.pack_params(stackp("m0"), stackp("S0"), stackp("A"), stackp("Q"), stackp("C"),
+                               stackp("offset"))
+    flags = batch.model_flags(stackp("A"), stackp("C"))
+    d = batch.make_time_major(st, dtype=np.float32)
+    r1 = batch.smooth(d, params, n=n, r=r, algo=1, flags=flags, want_nll=True, check=True)
+    o1 = r1["out"].cpu().numpy()
+    n1 = r1["nll"].cpu().numpy()
+    r2 = batch.smooth(d, params, n=n, r=r, algo=2, flags=flags, want_nll=True, check=True)
+    o2 = r2["out"].cpu().numpy()
+    n2 = r2["nll"].cpu().numpy()
+    assert np.abs(o1 - o2).max() < 1e-8
+    np.testing.assert_allclose(n2, n1, rtol=1e-10)
+    ref = _oracle_smooth_batch([st[0], st[B - 1]], [models[0], models[B - 1]], O)
+    assert np.abs(o2[0] - ref[0]).max() < OUT_TOL
+    assert np.abs(o2[B - 1] - ref[1]).max() < OUT_TOL
+
+
+def test_model_flag_violation_is_reported(torch):
+    from eks_amd import _lib, batch
+    st = np.random.default_rng(3).normal(100, 3, size=(2, 5, 300, 2))
+    A = np.array([[0.99, 0.0], [0.0, 1.0]])
+    params = batch.pack_params(np.zeros(2), np.eye(2) * 10, A, np.eye(2) * 0.1, np.eye(2),
+                               np.array([100.0, 100.0]))
+    params = params.expand(2, -1).contiguous()
+    res = batch.smooth(batch.make_time_major(st), params, n=2, r=2,
+                       flags=_lib.EKS_MODEL_A_IDENTITY | _lib.EKS_MODEL_C_IDENTITY)
+    assert ((res["status"] & _lib.EKS_STATUS_BAD_MODEL) != 0).all()
+    with pytest.raises(ValueError):
+        batch.smooth(batch.make_time_major(st), params, n=2, r=2, check=True,
+                     flags=_lib.EKS_MODEL_A_IDENTITY | _lib.EKS_MODEL_C_IDENTITY)
+
+
 def test_fused_edge_cases(torch):
     """T = 1, T = 2, zero-variance frames (all members agree) and NaN members."""
     from eks_amd import batch
     from oracle import eks_oracle as O
     rng = np.random.default_rng(7)
-    for T in (1, 2, 3, 64):
+    for T in (1, 2, 3, 64, 65, 200):
         st = rng.normal(100, 5, size=(1, 4, T, 2))
         st[0, :, 0, 0] = 42.0   # exact agreement -> R_00 = 0 at t = 0
         m = dict(m0=np.zeros(2), S0=np.diag([30.0, 20.0]), A=np.eye(2),
                  Q=np.array([[0.5, 0.1], [0.1, 0.4]]), C=np.eye(2), offset=np.array([100., 100.]))
         params = batch.pack_params(m["m0"], m["S0"], m["A"], m["Q"], m["C"], m["offset"])
-        res = batch.smooth(batch.make_time_major(st), params, n=2, r=2)
         ref = _oracle_smooth_batch([st[0]], [m], O)[0]
-        assert np.abs(res["out"][0].cpu().numpy() - ref).max() < OUT_TOL
+        for algo in (1, 2):
+            res = batch.smooth(batch.make_time_major(st), params, n=2, r=2, algo=algo)
+            assert np.abs(res["out"][0].cpu().numpy() - ref).max() < OUT_TOL, (T, algo)
     st = rng.normal(100, 5, size=(1, 5, 50, 2))
     st[0, 2, 20, 1] = np.nan
-    res = batch.smooth(batch.make_time_major(st), params, n=2, r=2)
-    out = res["out"][0].cpu().numpy()
     ref = _oracle_smooth_batch([st[0]], [m], O)[0]
-    np.testing.assert_array_equal(np.isnan(out), np.isnan(ref))
+    for algo in (1, 2):
+        res = batch.smooth(batch.make_time_major(st), params, n=2, r=2, algo=algo)
+        out = res["out"][0].cpu().numpy()
+        np.testing.assert_array_equal(np.isnan(out), np.isnan(ref))
 
 
 # -------------------------------------------------------------------------
