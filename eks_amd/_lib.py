@@ -43,7 +43,24 @@ SIGNATURES = {
     "eks_smooth": (_i32, [_p, _i32, _i64, _i64, _i32, _i32, _i32, _i64, _i64, _i64, _i64, _i32,
                           _p, _p, _i64, _i64, _i64, _p, _p, _p, _sz, _i32, _i32, _p, _p]),
     "eks_smooth_chunk_len": (_i64, [_i64, _i64, _i32]),
+    "eks_profile_begin": (_i32, [_i32]),
+    "eks_profile_end": (_i32, [_p, _p, _i32, _i32]),
 }
+
+
+def profile_begin(max_calls: int) -> None:
+    check(load().eks_profile_begin(max_calls), "eks_profile_begin")
+
+
+def profile_end(max_kernels: int = 8):
+    """[(kernel name, average ms per call)] for the profiled eks_smooth calls."""
+    ms = (C.c_double * max_kernels)()
+    names = C.create_string_buffer(64 * max_kernels)
+    k = load().eks_profile_end(ms, names, max_kernels, 64)
+    if k < 0:
+        check(k, "eks_profile_end")
+    raw = names.raw
+    return [(raw[i * 64:(i + 1) * 64].split(b"\0")[0].decode(), ms[i]) for i in range(k)]
 
 _lib = None
 

@@ -18,6 +18,13 @@ constexpr int kMaxMembers = 64; // E
 int set_err(int code, const char *fmt, ...);
 int check_launch(const char *what);
 
+// Optional per-kernel timing (eks_profile_begin/end): records a hipEvent on
+// the launch stream before each kernel of an eks_smooth call and after the
+// last one.  No-op unless profiling was switched on by the caller.
+void prof_mark(hipStream_t s, const char *next_kernel);
+void prof_call_begin();
+void prof_call_end(hipStream_t s);
+
 template <int R>
 EKS_DEV void load_vec(const double *p, double (&v)[R]) {
 #pragma unroll

@@ -22,6 +22,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <vector>
 #include <algorithm>
 
 #include "../../include/eks_hip.h"
@@ -45,6 +46,40 @@ int set_err(int code, const char *fmt, ...) {
   g_err = buf;
   return code;
 }
+
+// ------------------------------------------------------------------------
+// per-kernel timing of eks_smooth calls (profiling aid)
+// ------------------------------------------------------------------------
+struct Prof {
+  bool on = false;
+  int max_calls = 0, call = -1, mark = 0;
+  static constexpr int kMarks = 8;
+  std::vector<hipEvent_t> ev;
+  std::vector<int> nmarks;
+  std::vector<std::string> names;
+};
+static thread_local Prof g_prof;
+
+void prof_call_begin() {
+  if (!g_prof.on) return;
+  if (g_prof.call + 1 >= g_prof.max_calls) return;
+  ++g_prof.call;
+  g_prof.mark = 0;
+}
+
+void prof_mark(hipStream_t s, const char *next_kernel) {
+  if (!g_prof.on || g_prof.call < 0 || g_prof.call >= g_prof.max_calls) return;
+  if (g_prof.mark >= Prof::kMarks) return;
+  hipEventRecord(g_prof.ev[g_prof.call * Prof::kMarks + g_prof.mark], s);
+  if (g_prof.call == 0) {
+    if ((int)g_prof.names.size() <= g_prof.mark) g_prof.names.resize(g_prof.mark + 1);
+    g_prof.names[g_prof.mark] = next_kernel ? next_kernel : "";
+  }
+  ++g_prof.mark;
+  g_prof.nmarks[g_prof.call] = g_prof.mark;
+}
+
+void prof_call_end(hipStream_t s) { prof_mark(s, nullptr); }
 
 int check_launch(const char *what) {
   hipError_t e = hipGetLastError();
@@ -343,6 +378,52 @@ int eks_max_latent(void) { return kMaxLatent; }
 int eks_max_obs(void) { return kMaxObs; }
 int eks_max_members(void) { return kMaxMembers; }
 int64_t eks_param_len(int n, int r) { return param_len(n, r); }
+
+int eks_profile_begin(int max_calls) {
+  g_err.clear();
+  for (hipEvent_t e : g_prof.ev) hipEventDestroy(e);
+  g_prof = Prof();
+  if (max_calls <= 0) return EKS_OK;
+  g_prof.ev.resize((size_t)max_calls * Prof::kMarks);
+  for (auto &e : g_prof.ev)
+    if (hipEventCreate(&e) != hipSuccess) return set_err(EKS_ERR_HIP, "hipEventCreate failed");
+  g_prof.nmarks.assign(max_calls, 0);
+  g_prof.max_calls = max_calls;
+  g_prof.on = true;
+  return EKS_OK;
+}
+
+int eks_profile_end(double *kernel_ms, char *names, int max_kernels, int name_len) {
+  g_err.clear();
+  if (!g_prof.on) return set_err(EKS_ERR_ARG, "eks_profile_end: profiling not started");
+  const int calls = g_prof.call + 1;
+  int nk = 0;
+  for (int k = 0; k < max_kernels; ++k) kernel_ms[k] = 0.0;
+  for (int c = 0; c < calls; ++c) {
+    const int m = g_prof.nmarks[c];
+    if (m < 2) continue;
+    nk = std::max(nk, m - 1);
+    hipEvent_t *ev = &g_prof.ev[c * Prof::kMarks];
+    if (hipEventSynchronize(ev[m - 1]) != hipSuccess)
+      return set_err(EKS_ERR_HIP, "hipEventSynchronize failed");
+    for (int k = 0; k + 1 < m && k < max_kernels; ++k) {
+      float ms = 0.f;
+      hipEventElapsedTime(&ms, ev[k], ev[k + 1]);
+      kernel_ms[k] += ms;
+    }
+  }
+  if (names && name_len > 0) {
+    for (int k = 0; k < std::min(nk, max_kernels); ++k) {
+      const std::string &nm = k < (int)g_prof.names.size() ? g_prof.names[k] : std::string();
+      std::snprintf(names + (size_t)k * name_len, name_len, "%s", nm.c_str());
+    }
+  }
+  for (hipEvent_t e : g_prof.ev) hipEventDestroy(e);
+  const int ncalls = calls;
+  g_prof = Prof();
+  for (int k = 0; k < std::min(nk, max_kernels); ++k) kernel_ms[k] /= std::max(ncalls, 1);
+  return nk;
+}
 
 int eks_ensemble(const void *obs, int obs_dtype, int64_t B, int64_t T, int E, int n, int64_t sb,
                  int64_t st, int64_t se, int64_t sj, int mode, double *preds, double *vars,

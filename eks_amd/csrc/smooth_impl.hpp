@@ -623,8 +623,11 @@ int launch_shape(const SmoothArgs &a, int algo, long long L) {
       using Tp = decltype(tag);
       return dispatch_members_c(a.E, [&](auto Ec) {
         constexpr int EE = decltype(Ec)::value;
+        prof_call_begin();
+        prof_mark(a.stream, "k_smooth_seq");
         hipLaunchKernelGGL((k_smooth_seq<R, N, EE, Tp, AI, CI>), dim3(grid_for(a.B, 64)),
                            dim3(64), 0, a.stream, a);
+        prof_call_end(a.stream);
         return check_launch("k_smooth_seq");
       });
     };
@@ -637,15 +640,20 @@ int launch_shape(const SmoothArgs &a, int algo, long long L) {
   const bool y32 = f32 && a.median && (a.E == 3 || a.E == 5);
   auto rest = [&](auto ytag) -> int {
     using YT = decltype(ytag);
+    prof_mark(a.stream, "k_c2_fscan");
     hipLaunchKernelGGL((k_c2_fscan<R, N>), dim3(g64), dim3(64), 0, a.stream, a, p);
     if (int rc = check_launch("k_c2_fscan")) return rc;
+    prof_mark(a.stream, "k_c3_rerun");
     hipLaunchKernelGGL((k_c3_rerun<R, N, YT, AI, CI>), dim3(g256), dim3(256), 0, a.stream, a, p);
     if (int rc = check_launch("k_c3_rerun")) return rc;
+    prof_mark(a.stream, "k_c4_bscan");
     hipLaunchKernelGGL((k_c4_bscan<R>), dim3(g64), dim3(64), 0, a.stream, a, p);
     if (int rc = check_launch("k_c4_bscan")) return rc;
     constexpr int LS = R <= 2 ? 8 : 4;
+    prof_mark(a.stream, "k_c5_final");
     hipLaunchKernelGGL((k_c5_final<R, N, YT, AI, CI, LS>), dim3(g256), dim3(256), 0, a.stream, a,
                        p);
+    prof_call_end(a.stream);
     return check_launch("k_c5_final");
   };
   auto k1 = [&](auto tag, auto ytag) -> int {
@@ -653,6 +661,8 @@ int launch_shape(const SmoothArgs &a, int algo, long long L) {
     using YT = decltype(ytag);
     return dispatch_members_c(a.E, [&](auto Ec) {
       constexpr int EE = decltype(Ec)::value;
+      prof_call_begin();
+      prof_mark(a.stream, "k_c1_elem");
       hipLaunchKernelGGL((k_c1_elem<R, N, EE, Tp, YT, AI, CI>), dim3(g256), dim3(256), 0,
                          a.stream, a, p);
       return check_launch("k_c1_elem");

@@ -172,6 +172,18 @@ int eks_smooth(const void *obs, int obs_dtype, int64_t B, int64_t T, int E, int 
  * would be chosen automatically).  Exposed for tests and DESIGN.md. */
 int64_t eks_smooth_chunk_len(int64_t B, int64_t T, int r);
 
+/*
+ * Profiling aid (not part of the smoother's semantics).  After
+ * eks_profile_begin(max_calls), each eks_smooth call on this thread records
+ * a hipEvent on its stream before each of its kernels and after the last one
+ * (at most max_calls calls).  eks_profile_end synchronises on those events,
+ * writes the per-kernel average milliseconds over the recorded calls into
+ * kernel_ms[0..k) and the kernel names into names[k * name_len] (host
+ * buffers), switches profiling off and returns k (kernels per call).
+ */
+int eks_profile_begin(int max_calls);
+int eks_profile_end(double *kernel_ms, char *names, int max_kernels, int name_len);
+
 #ifdef __cplusplus
 }
 #endif
