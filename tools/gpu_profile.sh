@@ -1,13 +1,27 @@
 #!/bin/bash
 # rocprofv3 kernel-trace summary + HBM counters (separate --pmc passes, as
-# MI355X_MICROARCH.md prescribes) of the default bench workload.
+# MI355X_MICROARCH.md prescribes) of the default bench workload.  Raw
+# profiler output goes to /tmp on the box; only summaries are copied back.
 set -o pipefail
 export TMPDIR=/tmp PYTHONDONTWRITEBYTECODE=1
 TAG=${1:-r01}
+RAW=/tmp/prof_$TAG
 OUT=gpurun_out/prof_$TAG
-mkdir -p $OUT
-ARGS="--steps 5 --warmup 1 --no-cpu-baseline"
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 bench.py $ARGS > $OUT/bench_trace.log 2>&1 || exit $?
-timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 2 --warmup 0 --no-cpu-baseline > $OUT/pmc_fetch.log 2>&1 || exit $?
-timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o run --output-format csv -- python3 bench.py --steps 2 --warmup 0 --no-cpu-baseline > $OUT/pmc_write.log 2>&1 || exit $?
-find $OUT -name "*.csv" | head -50 > $OUT/files.txt
+mkdir -p $OUT $RAW
+step() {  # name, timeout, rocprof args...
+  local name=$1 t=$2; shift 2
+  timeout -k 10 $t rocprofv3 "$@" -d $RAW/$name -o run --output-format csv -- \
+      python3 bench.py --steps ${STEPS:-5} --warmup 1 --no-cpu-baseline > $OUT/$name.log 2>&1
+  local rc=$?
+  echo "$name rc=$rc" >> $OUT/status.txt
+  (cd $RAW && find $name -type f -printf "%s %p\n") >> $OUT/files.txt
+  for f in $(find $RAW/$name -name "*stats.csv" -o -name "*counter_collection.csv" -o -name "*agent_info.csv"); do
+    sz=$(stat -c %s "$f")
+    if [ "$sz" -lt 20000000 ]; then cp "$f" $OUT/${name}_$(basename $f); fi
+  done
+  return $rc
+}
+RX='k_c[0-9]|k_smooth_seq'
+step trace 600 --kernel-trace --stats || exit $?
+STEPS=2 step pmc_fetch 600 --kernel-include-regex "$RX" --pmc FETCH_SIZE || exit $?
+STEPS=2 step pmc_write 600 --kernel-include-regex "$RX" --pmc WRITE_SIZE || exit $?
