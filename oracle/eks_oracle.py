@@ -91,8 +91,8 @@ def kalman_dot(array, V, C, R):
 
     eks/ensemble_kalman.py:110-117 (LAPACK gesv through ``np.linalg.solve``).
     """
-    innov_cov = R + C @ (V @ C.T)
-    return V @ (C.T @ np.linalg.solve(innov_cov, array))
+    innov_cov = R + np.dot(C, np.dot(V, C.T))
+    return np.dot(V, np.dot(C.T, np.linalg.solve(innov_cov, array)))
 
 
 def filtering_pass(y, m0, S0, C, R, A, Q, ensemble_vars):
@@ -104,24 +104,26 @@ def filtering_pass(y, m0, S0, C, R, A, Q, ensemble_vars):
     *for* step t+1 (:101), and ``S[T-1]`` is never written (stays 0).
     """
     n_obs = ensemble_vars.shape[1]
-    diag = np.arange(n_obs)
     T = y.shape[0]
     r = m0.shape[0]
     mf = np.zeros((T, r))
     Vf = np.zeros((T, r, r))
     S = np.zeros((T, r, r))
-    R[diag, diag] = ensemble_vars[0]
-    mf[0] = m0 + kalman_dot(y[0] - C @ m0, S0, C, R)
-    Vf[0] = S0 - kalman_dot(C @ S0, S0, C, R)
+    for i in range(n_obs):
+        R[i, i] = ensemble_vars[0, i]
+    mf[0] = m0 + kalman_dot(y[0] - np.dot(C, m0), S0, C, R)
+    Vf[0] = S0 - kalman_dot(np.dot(C, S0), S0, C, R)
     S[0] = S0
     At = A.T
     for t in range(1, T):
-        R[diag, diag] = ensemble_vars[t]
-        prior_cov = A @ (Vf[t - 1] @ At) + Q
+        ev_t = ensemble_vars[t]
+        for i in range(n_obs):
+            R[i, i] = ev_t[i]
+        prior_cov = np.dot(A, np.dot(Vf[t - 1], At)) + Q
         S[t - 1] = prior_cov
-        prior_mean = A @ mf[t - 1]
-        mf[t] = prior_mean + kalman_dot(y[t] - C @ (A @ mf[t - 1]), prior_cov, C, R)
-        Vf[t] = prior_cov - kalman_dot(C @ prior_cov, prior_cov, C, R)
+        prior_mean = np.dot(A, mf[t - 1])
+        mf[t] = prior_mean + kalman_dot(y[t] - np.dot(C, prior_mean), prior_cov, C, R)
+        Vf[t] = prior_cov - kalman_dot(np.dot(C, prior_cov), prior_cov, C, R)
     return mf, Vf, S
 
 
@@ -139,10 +141,10 @@ def smooth_backward(y, mf, Vf, S, A, Q=None, C=None):
     ms[T - 1] = mf[T - 1]
     Vs[T - 1] = Vf[T - 1]
     for t in range(T - 2, -1, -1):
-        gain = np.linalg.solve(S[t], A @ Vf[t]).T  # :158
-        Vs[t] = Vf[t] + gain @ ((Vs[t + 1] - S[t]) @ gain.T)  # :160
-        ms[t] = mf[t] + gain @ (ms[t + 1] - A @ mf[t])  # :161
-        CV[t] = Vs[t + 1] @ gain.T  # :162
+        gain = np.linalg.solve(S[t], np.dot(A, Vf[t])).T  # :158
+        Vs[t] = Vf[t] + np.dot(gain, np.dot(Vs[t + 1] - S[t], gain.T))  # :160
+        ms[t] = mf[t] + np.dot(gain, ms[t + 1] - np.dot(A, mf[t]))  # :161
+        CV[t] = np.dot(Vs[t + 1], gain.T)  # :162
     return ms, Vs, CV
 
 
