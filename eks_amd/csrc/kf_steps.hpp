@@ -571,3 +571,110 @@ EKS_DEV bool compose_state(double (&m)[R], double (&P)[R][R], const Elem<R> &E) 
 }
 
 }  // namespace eks
+
+namespace eks {
+
+// Full associative composition of two filtering elements, i earlier than j
+// (Sarkka & Garcia-Fernandez 2021, Lemma 8):
+//   M = (I + Ci Jj)^-1
+//   A = Aj M Ai                      b = Aj M (bi + Ci eta_j) + bj
+//   C = Aj M Ci Aj^T + Cj            eta = Ai^T M^T (eta_j - Jj bi) + eta_i
+//   J = Ai^T M^T Jj Ai + Ji
+template <int R>
+EKS_DEV bool compose_elem(const Elem<R> &Ei, const Elem<R> &Ej, Elem<R> &out) {
+  double W[R][R], M[R][R];
+#pragma unroll
+  for (int i = 0; i < R; ++i)
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      double t = (i == j) ? 1.0 : 0.0;
+#pragma unroll
+      for (int k = 0; k < R; ++k) t = fma(Ei.Cb[i][k], Ej.Jb[k][j], t);
+      W[i][j] = t;
+      M[i][j] = (i == j) ? 1.0 : 0.0;
+    }
+  const bool ok = gauss_solve<R, R>(W, M);  // M = W^-1
+  double AjM[R][R], MAi[R][R];  // Aj M, and M Ai (whose transpose is Ai^T M^T)
+  matmul<R, R, R>(Ej.Ab, M, AjM);
+  matmul<R, R, R>(M, Ei.Ab, MAi);
+  // A = (Aj M) Ai
+  matmul<R, R, R>(AjM, Ei.Ab, out.Ab);
+  // b = (Aj M)(bi + Ci eta_j) + bj
+  double v[R];
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    double t = Ei.bb[i];
+#pragma unroll
+    for (int k = 0; k < R; ++k) t = fma(Ei.Cb[i][k], Ej.eta[k], t);
+    v[i] = t;
+  }
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    double t = Ej.bb[i];
+#pragma unroll
+    for (int k = 0; k < R; ++k) t = fma(AjM[i][k], v[k], t);
+    out.bb[i] = t;
+  }
+  // C = (Aj M) Ci Aj^T + Cj
+  double T1[R][R];
+  matmul<R, R, R>(AjM, Ei.Cb, T1);
+  double Cn[R][R];
+  matmul_nt<R, R, R>(T1, Ej.Ab, Cn);
+  // eta = (M Ai)^T (eta_j - Jj bi) + eta_i
+  double w[R];
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    double t = Ej.eta[i];
+#pragma unroll
+    for (int k = 0; k < R; ++k) t = fma(-Ej.Jb[i][k], Ei.bb[k], t);
+    w[i] = t;
+  }
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    double t = Ei.eta[i];
+#pragma unroll
+    for (int k = 0; k < R; ++k) t = fma(MAi[k][i], w[k], t);
+    out.eta[i] = t;
+  }
+  // J = (M Ai)^T Jj Ai + Ji
+  double T2[R][R], Jn[R][R];
+  matmul<R, R, R>(Ej.Jb, Ei.Ab, T2);
+#pragma unroll
+  for (int i = 0; i < R; ++i)
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      double t = Ei.Jb[i][j];
+#pragma unroll
+      for (int k = 0; k < R; ++k) t = fma(MAi[k][i], T2[k][j], t);
+      Jn[i][j] = t;
+    }
+#pragma unroll
+  for (int i = 0; i < R; ++i)
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      out.Cb[i][j] = 0.5 * ((Cn[i][j] + Ej.Cb[i][j]) + (Cn[j][i] + Ej.Cb[j][i]));
+      out.Jb[i][j] = 0.5 * (Jn[i][j] + Jn[j][i]);
+    }
+  return ok;
+}
+
+// Move a whole element between lanes of a wave (__shfl_up / __shfl_down).
+template <int R, bool UP>
+EKS_DEV Elem<R> shfl_elem(const Elem<R> &E, int delta) {
+  Elem<R> o;
+  auto mv = [&](double x) { return UP ? __shfl_up(x, delta, 64) : __shfl_down(x, delta, 64); };
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    o.bb[i] = mv(E.bb[i]);
+    o.eta[i] = mv(E.eta[i]);
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      o.Ab[i][j] = mv(E.Ab[i][j]);
+      o.Cb[i][j] = mv(E.Cb[i][j]);
+      o.Jb[i][j] = mv(E.Jb[i][j]);
+    }
+  }
+  return o;
+}
+
+}  // namespace eks

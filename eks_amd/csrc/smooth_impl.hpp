@@ -34,6 +34,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "../../include/eks_hip.h"
 #include "eks_common.hpp"
@@ -63,8 +64,30 @@ struct SmoothArgs {
   hipStream_t stream;
 };
 
-constexpr long long kTargetLanes = 256LL * 16 * 64;  // 4 waves per SIMD
+// Target number of (chunk, trajectory) lanes: enough 256-thread blocks that
+// the last partial round of resident blocks (the tail) is a small fraction of
+// the kernel.  EKS_TARGET_LANES overrides it (tuning experiments).
+constexpr long long kTargetLanesDefault = 256LL * 16 * 64;
 constexpr long long kMinChunk = 64;
+
+// above this many chunks per trajectory the chunk scans run one wave per
+// trajectory (EKS_WAVE_SCAN_CHUNKS overrides it: tuning and tests)
+inline long long wave_scan_chunks() {
+  static long long v = [] {
+    const char *e = getenv("EKS_WAVE_SCAN_CHUNKS");
+    return e ? atoll(e) : 24LL;
+  }();
+  return v;
+}
+
+inline long long target_lanes() {
+  static long long v = [] {
+    const char *e = getenv("EKS_TARGET_LANES");
+    long long x = e ? atoll(e) : 0;
+    return x > 0 ? x : kTargetLanesDefault;
+  }();
+  return v;
+}
 
 inline int sub_len(int r) { return r <= 2 ? 8 : 4; }
 inline int elem_len(int r) { return r * r + r + r * (r + 1) / 2 + r + r * (r + 1) / 2; }
@@ -74,7 +97,7 @@ inline long long round_up(long long x, long long m) { return (x + m - 1) / m * m
 
 inline long long chunk_len(long long B, long long T, int r) {
   const long long ls = sub_len(r);
-  const long long nc = std::max(1LL, (kTargetLanes + B - 1) / B);
+  const long long nc = std::max(1LL, (target_lanes() + B - 1) / B);
   long long L = std::max(kMinChunk, (T + nc - 1) / nc);
   L = round_up(L, ls);
   if (L >= T) L = round_up(T, ls);
@@ -281,76 +304,135 @@ __global__ __launch_bounds__(64) void k_smooth_seq(SmoothArgs a) {
 // ===========================================================================
 // algo 2 kernels
 // ===========================================================================
+// Lane mapping: a 256-thread block covers 256 consecutive trajectories of ONE
+// chunk, so the chunk index (and with it every time index and plane offset)
+// is wave-uniform and lives in SGPRs; the only per-lane address term is the
+// 32-bit trajectory index b (global_load saddr + voffset).
+constexpr int kBlock = 256;
+
+inline long long blocks_per_chunk(long long B) { return (B + kBlock - 1) / kBlock; }
+
 struct Lane {
-  long long c, b;
+  long long c;
+  unsigned b;
   EKS_DEV bool init(long long B, long long NC) {
-    const long long lane = blockIdx.x * (long long)blockDim.x + threadIdx.x;
-    if (lane >= NC * B) return false;
-    c = lane / B;
-    b = lane - c * B;
-    return true;
+    const long long bpc = (B + kBlock - 1) / kBlock;
+    c = blockIdx.x / bpc;
+    b = (unsigned)((blockIdx.x - c * bpc) * kBlock + threadIdx.x);
+    return c < NC && (long long)b < B;
   }
 };
 
-template <int R, int N, int E, typename T, typename YT, bool AI, bool CI>
-__global__ __launch_bounds__(256) void k_c1_elem(SmoothArgs a, ChunkPlan p) {
+// element `plane` of a time-major plane array (B values per plane): uniform
+// 64-bit plane base + 32-bit per-lane byte offset, which hipcc lowers to the
+// global_load/store saddr + voffset form (no per-lane 64-bit address math).
+template <typename T>
+EKS_DEV T &pl(T *base, long long plane, long long B, unsigned b) {
+  char *pb = (char *)(base + plane * B);
+  const unsigned off = b * (unsigned)sizeof(T);
+  return *(T *)(pb + off);
+}
+
+template <int R>
+EKS_DEV void store_state_pl(double *base, long long plane0, long long B, unsigned b,
+                            const double (&m)[R], const double (&P)[R][R]) {
+  int k = 0;
+#pragma unroll
+  for (int i = 0; i < R; ++i) pl(base, plane0 + (k++), B, b) = m[i];
+#pragma unroll
+  for (int i = 0; i < R; ++i)
+#pragma unroll
+    for (int j = i; j < R; ++j) pl(base, plane0 + (k++), B, b) = P[i][j];
+}
+
+template <int R>
+EKS_DEV void load_state_pl(const double *base, long long plane0, long long B, unsigned b,
+                           double (&m)[R], double (&P)[R][R]) {
+  int k = 0;
+#pragma unroll
+  for (int i = 0; i < R; ++i) m[i] = pl(base, plane0 + (k++), B, b);
+#pragma unroll
+  for (int i = 0; i < R; ++i)
+#pragma unroll
+    for (int j = i; j < R; ++j) P[i][j] = P[j][i] = pl(base, plane0 + (k++), B, b);
+}
+
+// Stream the chunk's member predictions once: ensemble each step, store the
+// raw average and the variance for K3/K5, and feed the step to `absorb`
+// (the plain filter for chunk 0, the element build otherwise).
+template <int E, int N, typename T, typename YT, int D, typename Absorb>
+EKS_DEV void c1_stream(const SmoothArgs &a, const ChunkPlan &p, long long s, long long e,
+                       unsigned b, const double (&off)[N], Absorb &&absorb) {
   constexpr int EE = E > 0 ? E : 1;
+  const long long B = a.B;
+  const bool median = a.median != 0;
+  YT *ybuf = (YT *)(a.ws + p.y_off);
+  double *evbuf = (double *)(a.ws + p.ev_off);
+  const T *ob = (const T *)a.obs + (long long)b * a.sb;
+  T ring[D][EE][N];
+  if constexpr (E > 0) {
+#pragma unroll
+    for (int q = 0; q < D; ++q)
+      if (s + q < e) load_step<E, N, T>(ob + (s + q) * a.st, a.se, a.sj, ring[q]);
+  }
+  for (long long t0 = s; t0 < e; t0 += D) {
+#pragma unroll
+    for (int q = 0; q < D; ++q) {
+      const long long t = t0 + q;
+      if (t < e) {
+        const T *pt = ob + t * a.st;
+        T cur[EE][N];
+        if constexpr (E > 0) {
+#pragma unroll
+          for (int u = 0; u < E; ++u)
+#pragma unroll
+            for (int j = 0; j < N; ++j) cur[u][j] = ring[q][u][j];
+          if (t + D < e) load_step<E, N, T>(pt + D * a.st, a.se, a.sj, ring[q]);
+        }
+        double avg[N], rv[N], y[N];
+        reduce_step<E, N, T>(cur, pt, a.se, a.sj, a.E, median, avg, rv);
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+          pl(ybuf, t * N + j, B, b) = (YT)avg[j];
+          pl(evbuf, t * N + j, B, b) = rv[j];
+          y[j] = avg[j] - off[j];
+        }
+        absorb(t, y, rv);
+      }
+    }
+  }
+}
+
+template <int R, int N, int E, typename T, typename YT, bool AI, bool CI>
+__global__ __launch_bounds__(kBlock) void k_c1_elem(SmoothArgs a, ChunkPlan p) {
+  constexpr int D = 2;  // member prefetch distance (steps)
   Lane ln;
   const long long B = a.B, TT = a.T;
   if (!ln.init(B, p.NC)) return;
-  const long long c = ln.c, b = ln.b;
-  const bool median = a.median != 0;
+  const long long c = ln.c;
+  const unsigned b = ln.b;
   Model<R, N> md;
-  md.load(a.params + b * ParamLayout<R, N>::len, c == 0);
-  if (c == 0 && !md.template valid<AI, CI>()) flag(a.status, b, EKS_STATUS_BAD_MODEL);
-  YT *ybuf = (YT *)(a.ws + p.y_off);
-  double *evbuf = (double *)(a.ws + p.ev_off);
+  md.load(a.params + (long long)b * ParamLayout<R, N>::len, c == 0);
   const long long s = c * p.L, e = min(TT, s + p.L);
-  const T *ob = (const T *)a.obs + b * a.sb;
   bool ok = true;
   Elem<R> El;
-  double m[R], P[R][R];
-  NllAcc acc;
   if (c == 0) {
+    if (!md.template valid<AI, CI>()) flag(a.status, b, EKS_STATUS_BAD_MODEL);
+    // chunk 0: the plain filter from the prior; summarised as the known
+    // filtered state (Ab = 0, bb = m, Cb = P, no likelihood terms)
+    double m[R], P[R][R];
+    NllAcc acc;
 #pragma unroll
     for (int i = 0; i < R; ++i) {
       m[i] = md.m0[i];
 #pragma unroll
       for (int j = 0; j < R; ++j) P[i][j] = md.S0[i][j];
     }
-  } else {
-    El.set_identity();
-  }
-  T cur[EE][N], nxt[EE][N];
-  if constexpr (E > 0) load_step<E, N, T>(ob + s * a.st, a.se, a.sj, cur);
-  for (long long t = s; t < e; ++t) {
-    const T *pt = ob + t * a.st;
-    if constexpr (E > 0) {
-      if (t + 1 < e) load_step<E, N, T>(pt + a.st, a.se, a.sj, nxt);
-    }
-    double avg[N], rv[N], y[N];
-    reduce_step<E, N, T>(cur, pt, a.se, a.sj, a.E, median, avg, rv);
-#pragma unroll
-    for (int j = 0; j < N; ++j) {
-      ybuf[(t * N + j) * B + b] = (YT)avg[j];
-      evbuf[(t * N + j) * B + b] = rv[j];
-      y[j] = avg[j] - md.off[j];
-    }
-    if (c == 0) {
+    c1_stream<E, N, T, YT, D>(a, p, s, e, b, md.off, [&](long long t, const double (&y)[N],
+                                                          const double (&rv)[N]) {
       if (t > 0) kf_predict<R, AI>(m, P, md.A, md.Q);
       kf_update<R, N, CI>(m, P, md.C, y, rv, acc, ok);
-    } else {
-      elem_absorb<R, N, AI, CI>(El, md.A, md.Q, md.C, y, rv, ok);
-    }
-    if constexpr (E > 0) {
-#pragma unroll
-      for (int q = 0; q < E; ++q)
-#pragma unroll
-        for (int j = 0; j < N; ++j) cur[q][j] = nxt[q][j];
-    }
-  }
-  if (c == 0) {
-    // chunk 0 summarised as the known filtered state: Ab = 0, bb = m, Cb = P
+    });
     El.set_identity();
 #pragma unroll
     for (int i = 0; i < R; ++i) {
@@ -361,6 +443,12 @@ __global__ __launch_bounds__(256) void k_c1_elem(SmoothArgs a, ChunkPlan p) {
         El.Cb[i][j] = P[i][j];
       }
     }
+  } else {
+    El.set_identity();
+    c1_stream<E, N, T, YT, D>(a, p, s, e, b, md.off, [&](long long, const double (&y)[N],
+                                                          const double (&rv)[N]) {
+      elem_absorb<R, N, AI, CI>(El, md.A, md.Q, md.C, y, rv, ok);
+    });
   }
   El.store((double *)(a.ws + p.elem_off) + (c * Elem<R>::len) * B + b, B);
   if (!ok) flag(a.status, b, c == 0 ? EKS_STATUS_SINGULAR : EKS_STATUS_SCAN);
@@ -401,31 +489,208 @@ __global__ __launch_bounds__(64) void k_c2_fscan(SmoothArgs a, ChunkPlan p) {
   if (!ok) flag(a.status, b, EKS_STATUS_SCAN);
 }
 
-// y / ev of step t (time-major planes) with the centring offset applied
-template <int N, typename YT>
-EKS_DEV void read_yev(const YT *ybuf, const double *evbuf, long long t, long long B, long long b,
-                      const double (&off)[N], double (&y)[N], double (&rv)[N]) {
+// K2, wave-parallel form: one wave per trajectory for many chunks.  Lane l
+// owns chunks [l q, (l+1) q): it composes their elements, the wave scans the
+// 64 aggregates (Hillis-Steele, log2 64 = 6 compositions), and each lane then
+// walks its chunks from its exclusive prefix.  Latency O(q + 6 + q) element
+// compositions instead of O(NC).
+template <int R, int N>
+__global__ __launch_bounds__(64) void k_c2_fscan_w(SmoothArgs a, ChunkPlan p) {
+  const long long b = blockIdx.x;
+  const int l = threadIdx.x;
+  const long long B = a.B, NC = p.NC;
+  if (b >= B) return;
+  constexpr int KS = R + Sym<R>::len;
+  const double *elem = (const double *)(a.ws + p.elem_off);
+  double *cst = (double *)(a.ws + p.cstart_off);
+  const long long q = (NC + 63) / 64;
+  const long long c0 = min(NC, (long long)l * q), c1 = min(NC, c0 + q);
+  bool ok = true;
+  Elem<R> agg;
+  agg.set_identity();
+  for (long long c = c0; c < c1; ++c) {
+    Elem<R> e;
+    e.load(elem + (c * Elem<R>::len) * B + b, B);
+    Elem<R> t;
+    ok = compose_elem<R>(agg, e, t) && ok;
+    agg = t;
+  }
 #pragma unroll
-  for (int j = 0; j < N; ++j) {
-    y[j] = (double)ybuf[(t * N + j) * B + b] - off[j];
-    rv[j] = evbuf[(t * N + j) * B + b];
+  for (int k = 1; k < 64; k <<= 1) {
+    const Elem<R> o = shfl_elem<R, true>(agg, k);
+    if (l >= k) {
+      Elem<R> t;
+      ok = compose_elem<R>(o, agg, t) && ok;
+      agg = t;
+    }
+  }
+  const Elem<R> ex = shfl_elem<R, true>(agg, 1);
+  if (c0 < c1) {
+    double m[R], P[R][R];
+    long long c = c0;
+    if (l == 0) {
+      using L = ParamLayout<R, N>;
+      const double *pp = a.params + b * L::len;
+      load_vec<R>(pp + L::m0, m);
+      load_mat<R, R>(pp + L::S0, P);
+      store_state<R>(cst + b, B, m, P);  // chunk 0 starts from the prior
+      Elem<R> e0;
+      e0.load(elem + b, B);
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        m[i] = e0.bb[i];
+#pragma unroll
+        for (int j = 0; j < R; ++j) P[i][j] = e0.Cb[i][j];
+      }
+      c = 1;
+    } else {
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        m[i] = ex.bb[i];
+#pragma unroll
+        for (int j = 0; j < R; ++j) P[i][j] = ex.Cb[i][j];
+      }
+    }
+    for (; c < c1; ++c) {
+      store_state<R>(cst + (c * KS) * B + b, B, m, P);
+      if (c + 1 < c1) {
+        Elem<R> e;
+        e.load(elem + (c * Elem<R>::len) * B + b, B);
+        ok = compose_state<R>(m, P, e) && ok;
+      }
+    }
+  }
+  if (!ok) flag(a.status, b, EKS_STATUS_SCAN);
+}
+
+template <int R>
+struct Affine {
+  double G[R][R], g[R];
+  EKS_DEV void set_identity() {
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      g[i] = 0.0;
+#pragma unroll
+      for (int j = 0; j < R; ++j) G[i][j] = (i == j) ? 1.0 : 0.0;
+    }
+  }
+  // (this o h)(x) = G (Gh x + gh) + g
+  EKS_DEV Affine after(const Affine &h) const {
+    Affine o;
+    matmul<R, R, R>(G, h.G, o.G);
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      double t = g[i];
+#pragma unroll
+      for (int k = 0; k < R; ++k) t = fma(G[i][k], h.g[k], t);
+      o.g[i] = t;
+    }
+    return o;
+  }
+  EKS_DEV Affine shfl_down(int delta) const {
+    Affine o;
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      o.g[i] = __shfl_down(g[i], delta, 64);
+#pragma unroll
+      for (int j = 0; j < R; ++j) o.G[i][j] = __shfl_down(G[i][j], delta, 64);
+    }
+    return o;
+  }
+};
+
+// K4, wave-parallel form: chunk maps ms_start[c] = G_c ms_start[c+1] + g_c
+// composed right-to-left per lane, a suffix scan over lanes, then each lane
+// walks its chunks; NLL shares summed by a wave reduction.
+template <int R>
+__global__ __launch_bounds__(64) void k_c4_bscan_w(SmoothArgs a, ChunkPlan p) {
+  const long long b = blockIdx.x;
+  const int l = threadIdx.x;
+  const long long B = a.B, NC = p.NC;
+  if (b >= B) return;
+  const double *bw = (const double *)(a.ws + p.bwd_off);
+  double *msend = (double *)(a.ws + p.msend_off);
+  const long long q = (NC + 63) / 64;
+  const long long c0 = min(NC, (long long)l * q), c1 = min(NC, c0 + q);
+  auto load_map = [&](long long c) {
+    Affine<R> f;
+    const double *s = bw + (c * (R * R + R)) * B + b;
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      f.g[i] = s[(R * R + i) * B];
+#pragma unroll
+      for (int j = 0; j < R; ++j) f.G[i][j] = s[(i * R + j) * B];
+    }
+    return f;
+  };
+  Affine<R> F;
+  F.set_identity();
+  for (long long c = c1 - 1; c >= c0; --c) F = load_map(c).after(F);
+#pragma unroll
+  for (int k = 1; k < 64; k <<= 1) {
+    const Affine<R> o = F.shfl_down(k);
+    if (l + k < 64) F = F.after(o);
+  }
+  Affine<R> X = F.shfl_down(1);
+  if (l == 63) X.set_identity();
+  double ms[R];
+#pragma unroll
+  for (int i = 0; i < R; ++i) ms[i] = X.g[i];
+  for (long long c = c1 - 1; c >= c0; --c) {
+    if (c + 1 < NC) {
+#pragma unroll
+      for (int i = 0; i < R; ++i) msend[(c * R + i) * B + b] = ms[i];
+    }
+    const Affine<R> f = load_map(c);
+    double nx[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      double t = f.g[i];
+#pragma unroll
+      for (int k = 0; k < R; ++k) t = fma(f.G[i][k], ms[k], t);
+      nx[i] = t;
+    }
+#pragma unroll
+    for (int i = 0; i < R; ++i) ms[i] = nx[i];
+  }
+  if (a.nll) {
+    const double *np_ = (const double *)(a.ws + p.nllp_off);
+    double s = 0.0;
+    for (long long c = c0; c < c1; ++c) s += np_[c * B + b];
+#pragma unroll
+    for (int k = 32; k >= 1; k >>= 1) s += __shfl_xor(s, k, 64);
+    if (l == 0) a.nll[b] = s;
   }
 }
 
-template <int R, int N, typename YT, bool AI, bool CI>
-__global__ __launch_bounds__(256) void k_c3_rerun(SmoothArgs a, ChunkPlan p) {
+// y / ev of step t (time-major planes), raw
+template <int N, typename YT>
+EKS_DEV void load_yev(const YT *ybuf, const double *evbuf, long long t, long long B, unsigned b,
+                      YT (&y)[N], double (&rv)[N]) {
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    y[j] = pl(ybuf, t * N + j, B, b);
+    rv[j] = pl(evbuf, t * N + j, B, b);
+  }
+}
+
+template <int R, int N, typename YT, bool AI, bool CI, int LS>
+__global__ __launch_bounds__(kBlock) void k_c3_rerun(SmoothArgs a, ChunkPlan p) {
+  constexpr int D = 4;  // y / ev prefetch distance (steps); divides LS
+  static_assert(LS % D == 0, "prefetch distance must divide the checkpoint interval");
   Lane ln;
   const long long B = a.B, TT = a.T;
   if (!ln.init(B, p.NC)) return;
-  const long long c = ln.c, b = ln.b;
+  const long long c = ln.c;
+  const unsigned b = ln.b;
   constexpr int KS = R + Sym<R>::len;
   Model<R, N> md;
-  md.load(a.params + b * ParamLayout<R, N>::len, false);
+  md.load(a.params + (long long)b * ParamLayout<R, N>::len, false);
   const YT *ybuf = (const YT *)(a.ws + p.y_off);
   const double *evbuf = (const double *)(a.ws + p.ev_off);
-  double *ckpt = (double *)(a.ws + p.ckpt_off) + (c * p.NSUB * KS) * B + b;
+  double *ckpt = (double *)(a.ws + p.ckpt_off);
   double m[R], P[R][R];
-  load_state<R>((const double *)(a.ws + p.cstart_off) + (c * KS) * B + b, B, m, P);
+  load_state_pl<R>((const double *)(a.ws + p.cstart_off), c * KS, B, b, m, P);
   const long long s = c * p.L, e = min(TT, s + p.L);
   double G[R][R], g[R];
 #pragma unroll
@@ -436,60 +701,66 @@ __global__ __launch_bounds__(256) void k_c3_rerun(SmoothArgs a, ChunkPlan p) {
   }
   bool ok = true;
   NllAcc acc;
-  int sub = 0, k = 0;
-  double y[N], rv[N], yn[N], rvn[N];
-  read_yev<N, YT>(ybuf, evbuf, s, B, b, md.off, y, rv);
-  for (long long t = s; t < e; ++t) {
-    if (t + 1 < e) read_yev<N, YT>(ybuf, evbuf, t + 1, B, b, md.off, yn, rvn);
-    if (sub == 0) store_state<R>(ckpt + (k * KS) * B, B, m, P);
-    if (t > 0) kf_predict<R, AI>(m, P, md.A, md.Q);
-    kf_update<R, N, CI>(m, P, md.C, y, rv, acc, ok);
-    if (t + 1 < TT) {
-      double J[R][R], d[R], GJ[R][R];
-      ok = rts_gain<R, AI>(m, P, md.A, md.Q, J, d) && ok;
+  YT yr[D][N];
+  double er[D][N];
 #pragma unroll
-      for (int i = 0; i < R; ++i) {
-        double sg = g[i];
+  for (int q = 0; q < D; ++q)
+    if (s + q < e) load_yev<N, YT>(ybuf, evbuf, s + q, B, b, yr[q], er[q]);
+  long long k = 0;
+  for (long long t0 = s; t0 < e; t0 += LS, ++k) {
+    store_state_pl<R>(ckpt, (c * p.NSUB + k) * KS, B, b, m, P);  // state before t0
 #pragma unroll
-        for (int q = 0; q < R; ++q) sg = fma(G[i][q], d[q], sg);
-        g[i] = sg;
+    for (int q = 0; q < LS; ++q) {
+      const long long t = t0 + q;
+      if (t < e) {
+        double y[N], rv[N];
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+          y[j] = (double)yr[q % D][j] - md.off[j];
+          rv[j] = er[q % D][j];
+        }
+        if (t + D < e) load_yev<N, YT>(ybuf, evbuf, t + D, B, b, yr[q % D], er[q % D]);
+        if (t > 0) kf_predict<R, AI>(m, P, md.A, md.Q);
+        kf_update<R, N, CI>(m, P, md.C, y, rv, acc, ok);
+        if (t + 1 < TT) {
+          double J[R][R], d[R], GJ[R][R];
+          ok = rts_gain<R, AI>(m, P, md.A, md.Q, J, d) && ok;
+#pragma unroll
+          for (int i = 0; i < R; ++i) {
+            double sg = g[i];
+#pragma unroll
+            for (int u = 0; u < R; ++u) sg = fma(G[i][u], d[u], sg);
+            g[i] = sg;
+          }
+          matmul<R, R, R>(G, J, GJ);
+#pragma unroll
+          for (int i = 0; i < R; ++i)
+#pragma unroll
+            for (int j = 0; j < R; ++j) G[i][j] = GJ[i][j];
+        } else {  // ms[T-1] = mf[T-1]: the map ends in a constant
+#pragma unroll
+          for (int i = 0; i < R; ++i) {
+            double sg = g[i];
+#pragma unroll
+            for (int u = 0; u < R; ++u) sg = fma(G[i][u], m[u], sg);
+            g[i] = sg;
+          }
+#pragma unroll
+          for (int i = 0; i < R; ++i)
+#pragma unroll
+            for (int j = 0; j < R; ++j) G[i][j] = 0.0;
+        }
       }
-      matmul<R, R, R>(G, J, GJ);
-#pragma unroll
-      for (int i = 0; i < R; ++i)
-#pragma unroll
-        for (int j = 0; j < R; ++j) G[i][j] = GJ[i][j];
-    } else {  // ms[T-1] = mf[T-1]: the map ends in a constant
-#pragma unroll
-      for (int i = 0; i < R; ++i) {
-        double sg = g[i];
-#pragma unroll
-        for (int q = 0; q < R; ++q) sg = fma(G[i][q], m[q], sg);
-        g[i] = sg;
-      }
-#pragma unroll
-      for (int i = 0; i < R; ++i)
-#pragma unroll
-        for (int j = 0; j < R; ++j) G[i][j] = 0.0;
-    }
-#pragma unroll
-    for (int j = 0; j < N; ++j) {
-      y[j] = yn[j];
-      rv[j] = rvn[j];
-    }
-    if (++sub == p.LS) {
-      sub = 0;
-      ++k;
     }
   }
-  double *bw = (double *)(a.ws + p.bwd_off) + (c * (R * R + R)) * B + b;
+  double *bw = (double *)(a.ws + p.bwd_off);
 #pragma unroll
   for (int i = 0; i < R; ++i)
 #pragma unroll
-    for (int j = 0; j < R; ++j) bw[(i * R + j) * B] = G[i][j];
+    for (int j = 0; j < R; ++j) pl(bw, c * (R * R + R) + i * R + j, B, b) = G[i][j];
 #pragma unroll
-  for (int i = 0; i < R; ++i) bw[(R * R + i) * B] = g[i];
-  ((double *)(a.ws + p.nllp_off))[c * B + b] = acc.value((double)(e - s) * N);
+  for (int i = 0; i < R; ++i) pl(bw, c * (R * R + R) + R * R + i, B, b) = g[i];
+  pl((double *)(a.ws + p.nllp_off), c, B, b) = acc.value((double)(e - s) * N);
   if (!ok) flag(a.status, b, EKS_STATUS_SINGULAR);
 }
 
@@ -529,43 +800,52 @@ __global__ __launch_bounds__(64) void k_c4_bscan(SmoothArgs a, ChunkPlan p) {
 }
 
 template <int R, int N, typename YT, bool AI, bool CI, int LS>
-__global__ __launch_bounds__(256) void k_c5_final(SmoothArgs a, ChunkPlan p) {
+__global__ __launch_bounds__(kBlock) void k_c5_final(SmoothArgs a, ChunkPlan p) {
   Lane ln;
   const long long B = a.B, TT = a.T;
   if (!ln.init(B, p.NC)) return;
-  const long long c = ln.c, b = ln.b;
+  const long long c = ln.c;
+  const unsigned b = ln.b;
   constexpr int KS = R + Sym<R>::len;
   Model<R, N> md;
-  md.load(a.params + b * ParamLayout<R, N>::len, false);
+  md.load(a.params + (long long)b * ParamLayout<R, N>::len, false);
   const YT *ybuf = (const YT *)(a.ws + p.y_off);
   const double *evbuf = (const double *)(a.ws + p.ev_off);
-  const double *ckpt = (const double *)(a.ws + p.ckpt_off) + (c * p.NSUB * KS) * B + b;
+  const double *ckpt = (const double *)(a.ws + p.ckpt_off);
   double ms[R];
   if (c + 1 < p.NC) {
     const double *me = (const double *)(a.ws + p.msend_off);
 #pragma unroll
-    for (int i = 0; i < R; ++i) ms[i] = me[(c * R + i) * B + b];
+    for (int i = 0; i < R; ++i) ms[i] = pl(me, c * R + i, B, b);
   } else {
 #pragma unroll
     for (int i = 0; i < R; ++i) ms[i] = 0.0;
   }
   const long long s = c * p.L, e = min(TT, s + p.L);
-  const int nsub = (int)((e - s + LS - 1) / LS);
+  const long long nsub = (e - s + LS - 1) / LS;
   bool ok = true;
   NllAcc dummy;
-  double *outb = a.out + b * a.ob;
-  for (int k = nsub - 1; k >= 0; --k) {
-    const long long t0 = s + (long long)k * LS;
-    const int cnt = (int)min((long long)LS, e - t0);
+  double *outb = a.out + (long long)b * a.ob;
+  for (long long k = nsub - 1; k >= 0; --k) {
+    const long long t0 = s + k * LS;
     double m[R], P[R][R];
-    load_state<R>(ckpt + (k * KS) * B, B, m, P);
+    load_state_pl<R>(ckpt, (c * p.NSUB + k) * KS, B, b, m, P);
+    YT yr[LS][N];
+    double er[LS][N];
+#pragma unroll
+    for (int j = 0; j < LS; ++j)
+      if (t0 + j < e) load_yev<N, YT>(ybuf, evbuf, t0 + j, B, b, yr[j], er[j]);
     double Jr[LS][R][R], dr[LS][R];
 #pragma unroll
     for (int j = 0; j < LS; ++j) {
-      if (j < cnt) {
-        const long long t = t0 + j;
+      const long long t = t0 + j;
+      if (t < e) {
         double y[N], rv[N];
-        read_yev<N, YT>(ybuf, evbuf, t, B, b, md.off, y, rv);
+#pragma unroll
+        for (int q = 0; q < N; ++q) {
+          y[q] = (double)yr[j][q] - md.off[q];
+          rv[q] = er[j][q];
+        }
         if (t > 0) kf_predict<R, AI>(m, P, md.A, md.Q);
         kf_update<R, N, CI>(m, P, md.C, y, rv, dummy, ok);
         if (t + 1 < TT) {
@@ -582,8 +862,8 @@ __global__ __launch_bounds__(256) void k_c5_final(SmoothArgs a, ChunkPlan p) {
     }
 #pragma unroll
     for (int j = LS - 1; j >= 0; --j) {
-      if (j < cnt) {
-        const long long t = t0 + j;
+      const long long t = t0 + j;
+      if (t < e) {
         double nx[R];
 #pragma unroll
         for (int i = 0; i < R; ++i) {
@@ -595,7 +875,7 @@ __global__ __launch_bounds__(256) void k_c5_final(SmoothArgs a, ChunkPlan p) {
 #pragma unroll
         for (int i = 0; i < R; ++i) ms[i] = nx[i];
         project_store<R, N, CI>(outb + t * a.ot, a.oj, md.C, ms, md.off);
-        if (a.ms) store_vec<R>(a.ms + (b * TT + t) * R, ms);
+        if (a.ms) store_vec<R>(a.ms + ((long long)b * TT + t) * R, ms);
       }
     }
   }
@@ -634,25 +914,36 @@ int launch_shape(const SmoothArgs &a, int algo, long long L) {
     return f32 ? go(float{}) : go(double{});
   }
   const ChunkPlan p = make_plan(a.B, a.T, R, N, L);
-  const unsigned g256 = grid_for(p.NC * a.B, 256);
+  const unsigned g256 = (unsigned)(p.NC * blocks_per_chunk(a.B));
   const unsigned g64 = grid_for(a.B, 64);
   // y is stored as float when it is exactly a member value (odd-E median of f32)
   const bool y32 = f32 && a.median && (a.E == 3 || a.E == 5);
   auto rest = [&](auto ytag) -> int {
     using YT = decltype(ytag);
+    // the chunk scans: one lane per trajectory while the chain is short, one
+    // wave per trajectory (log-depth scan) when it is long
+    const bool wave_scan = p.NC > wave_scan_chunks();
     prof_mark(a.stream, "k_c2_fscan");
-    hipLaunchKernelGGL((k_c2_fscan<R, N>), dim3(g64), dim3(64), 0, a.stream, a, p);
+    if (wave_scan)
+      hipLaunchKernelGGL((k_c2_fscan_w<R, N>), dim3((unsigned)a.B), dim3(64), 0, a.stream, a, p);
+    else
+      hipLaunchKernelGGL((k_c2_fscan<R, N>), dim3(g64), dim3(64), 0, a.stream, a, p);
     if (int rc = check_launch("k_c2_fscan")) return rc;
     prof_mark(a.stream, "k_c3_rerun");
-    hipLaunchKernelGGL((k_c3_rerun<R, N, YT, AI, CI>), dim3(g256), dim3(256), 0, a.stream, a, p);
+    constexpr int LS3 = R <= 2 ? 8 : 4;
+    hipLaunchKernelGGL((k_c3_rerun<R, N, YT, AI, CI, LS3>), dim3(g256), dim3(kBlock), 0, a.stream,
+                       a, p);
     if (int rc = check_launch("k_c3_rerun")) return rc;
     prof_mark(a.stream, "k_c4_bscan");
-    hipLaunchKernelGGL((k_c4_bscan<R>), dim3(g64), dim3(64), 0, a.stream, a, p);
+    if (wave_scan)
+      hipLaunchKernelGGL((k_c4_bscan_w<R>), dim3((unsigned)a.B), dim3(64), 0, a.stream, a, p);
+    else
+      hipLaunchKernelGGL((k_c4_bscan<R>), dim3(g64), dim3(64), 0, a.stream, a, p);
     if (int rc = check_launch("k_c4_bscan")) return rc;
     constexpr int LS = R <= 2 ? 8 : 4;
     prof_mark(a.stream, "k_c5_final");
-    hipLaunchKernelGGL((k_c5_final<R, N, YT, AI, CI, LS>), dim3(g256), dim3(256), 0, a.stream, a,
-                       p);
+    hipLaunchKernelGGL((k_c5_final<R, N, YT, AI, CI, LS>), dim3(g256), dim3(kBlock), 0, a.stream,
+                       a, p);
     prof_call_end(a.stream);
     return check_launch("k_c5_final");
   };
@@ -663,7 +954,7 @@ int launch_shape(const SmoothArgs &a, int algo, long long L) {
       constexpr int EE = decltype(Ec)::value;
       prof_call_begin();
       prof_mark(a.stream, "k_c1_elem");
-      hipLaunchKernelGGL((k_c1_elem<R, N, EE, Tp, YT, AI, CI>), dim3(g256), dim3(256), 0,
+      hipLaunchKernelGGL((k_c1_elem<R, N, EE, Tp, YT, AI, CI>), dim3(g256), dim3(kBlock), 0,
                          a.stream, a, p);
       return check_launch("k_c1_elem");
     });
