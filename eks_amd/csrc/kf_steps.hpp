@@ -247,10 +247,12 @@ EKS_DEV void kf_update(double (&m)[R], double (&P)[R][R], const double (&C)[N][R
   acc.renorm();
 }
 
-// Inverse of a symmetric positive definite R x R matrix (closed form for
-// R <= 2, Gauss-Jordan with partial pivoting above).  false if singular.
+// Inverse of a small R x R matrix: adjugate / determinant (one reciprocal,
+// short dependency chain) for R <= 3, Gauss-Jordan with partial pivoting
+// above.  Used on well-conditioned matrices (S = A P A^T + Q, I + P J with
+// P, J positive semi-definite).  false if singular.
 template <int R>
-EKS_DEV bool spd_inverse(const double (&S)[R][R], double (&Si)[R][R]) {
+EKS_DEV bool small_inverse(const double (&S)[R][R], double (&Si)[R][R]) {
   if constexpr (R == 1) {
     Si[0][0] = rcp_nr(S[0][0]);
     return S[0][0] != 0.0;
@@ -314,7 +316,7 @@ EKS_DEV bool rts_gain(const double (&m)[R], const double (&P)[R][R], const doubl
 #pragma unroll
       for (int j = 0; j < R; ++j) S[i][j] += Q[i][j];
   }
-  const bool ok = spd_inverse<R>(S, Si);
+  const bool ok = small_inverse<R>(S, Si);
   matmul<R, R, R>(PAt, Si, J);
   double Am[R];
   if constexpr (AI) {
@@ -526,13 +528,13 @@ EKS_DEV void elem_absorb(Elem<R> &E, const double (&A)[R][R], const double (&Q)[
 //   P' = Ab (I + P Jb)^-1 P Ab^T + Cb,   m' = Ab (I + P Jb)^-1 (m + P eta) + bb
 template <int R>
 EKS_DEV bool compose_state(double (&m)[R], double (&P)[R][R], const Elem<R> &E) {
-  double M[R][R], X[R][1 + R];
+  double W[R][R], Mi[R][R], v[R], PAt[R][R];
 #pragma unroll
   for (int i = 0; i < R; ++i) {
     double pe = m[i];
 #pragma unroll
     for (int k = 0; k < R; ++k) pe = fma(P[i][k], E.eta[k], pe);
-    X[i][0] = pe;
+    v[i] = pe;
 #pragma unroll
     for (int j = 0; j < R; ++j) {
       double t = (i == j) ? 1.0 : 0.0, u = 0.0;
@@ -541,16 +543,19 @@ EKS_DEV bool compose_state(double (&m)[R], double (&P)[R][R], const Elem<R> &E) 
         t = fma(P[i][k], E.Jb[k][j], t);
         u = fma(P[i][k], E.Ab[j][k], u);
       }
-      M[i][j] = t;
-      X[i][1 + j] = u;
+      W[i][j] = t;
+      PAt[i][j] = u;
     }
   }
-  const bool ok = gauss_solve<R, 1 + R>(M, X);
+  const bool ok = small_inverse<R>(W, Mi);  // (I + P Jb)^-1
+  double x0[R], XP[R][R];
+  matvec<R, R>(Mi, v, x0);
+  matmul<R, R, R>(Mi, PAt, XP);
 #pragma unroll
   for (int i = 0; i < R; ++i) {
     double s = E.bb[i];
 #pragma unroll
-    for (int k = 0; k < R; ++k) s = fma(E.Ab[i][k], X[k][0], s);
+    for (int k = 0; k < R; ++k) s = fma(E.Ab[i][k], x0[k], s);
     m[i] = s;
   }
   double Pn[R][R];
@@ -560,7 +565,7 @@ EKS_DEV bool compose_state(double (&m)[R], double (&P)[R][R], const Elem<R> &E) 
     for (int j = 0; j < R; ++j) {
       double s = E.Cb[i][j];
 #pragma unroll
-      for (int k = 0; k < R; ++k) s = fma(E.Ab[i][k], X[k][1 + j], s);
+      for (int k = 0; k < R; ++k) s = fma(E.Ab[i][k], XP[k][j], s);
       Pn[i][j] = s;
     }
 #pragma unroll
@@ -593,7 +598,7 @@ EKS_DEV bool compose_elem(const Elem<R> &Ei, const Elem<R> &Ej, Elem<R> &out) {
       W[i][j] = t;
       M[i][j] = (i == j) ? 1.0 : 0.0;
     }
-  const bool ok = gauss_solve<R, R>(W, M);  // M = W^-1
+  const bool ok = small_inverse<R>(W, M);  // M = W^-1
   double AjM[R][R], MAi[R][R];  // Aj M, and M Ai (whose transpose is Ai^T M^T)
   matmul<R, R, R>(Ej.Ab, M, AjM);
   matmul<R, R, R>(M, Ei.Ab, MAi);

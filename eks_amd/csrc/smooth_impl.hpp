@@ -11,7 +11,8 @@
 // intermediates below is one coalesced 256..512-byte access per wave.
 //
 //  K1 k_c1_elem    members -> ensemble (median, var/E) -> y (raw), ev stored
-//                  time-major; builds the chunk's filtering element
+//                  time-major; builds the chunk's filtering element (stored
+//                  trajectory-major, one row per (b, c), for the scans)
 //                  (kf_steps.hpp, Elem) or, for chunk 0, runs the plain filter
 //  K2 k_c2_fscan   per trajectory, sequential over chunks: filtered state at
 //                  every chunk start (state (x) element composition)
@@ -450,7 +451,7 @@ __global__ __launch_bounds__(kBlock) void k_c1_elem(SmoothArgs a, ChunkPlan p) {
       elem_absorb<R, N, AI, CI>(El, md.A, md.Q, md.C, y, rv, ok);
     });
   }
-  El.store((double *)(a.ws + p.elem_off) + (c * Elem<R>::len) * B + b, B);
+  El.store((double *)(a.ws + p.elem_off) + ((long long)b * p.NC + c) * Elem<R>::len, 1);
   if (!ok) flag(a.status, b, c == 0 ? EKS_STATUS_SINGULAR : EKS_STATUS_SCAN);
 }
 
@@ -470,8 +471,10 @@ __global__ __launch_bounds__(64) void k_c2_fscan(SmoothArgs a, ChunkPlan p) {
     load_mat<R, R>(pp + L::S0, P);
     store_state<R>(cst + b, B, m, P);  // chunk 0 starts from the prior
   }
-  Elem<R> El;
-  El.load(elem + b, B);
+  Elem<R> El, Nx;
+  // elements are stored trajectory-major: row (b, c) of Elem<R>::len doubles
+  const double *erow = elem + b * p.NC * Elem<R>::len;
+  El.load(erow, 1);
 #pragma unroll
   for (int i = 0; i < R; ++i) {
     m[i] = El.bb[i];
@@ -479,11 +482,15 @@ __global__ __launch_bounds__(64) void k_c2_fscan(SmoothArgs a, ChunkPlan p) {
     for (int j = 0; j < R; ++j) P[i][j] = El.Cb[i][j];
   }
   bool ok = true;
+  // software pipelined: the element of chunk c+1 is in flight while chunk c
+  // is composed (the chain is latency bound, not bandwidth bound)
+  if (p.NC > 1) El.load(erow + Elem<R>::len, 1);
   for (long long c = 1; c < p.NC; ++c) {
     store_state<R>(cst + (c * KS) * B + b, B, m, P);
     if (c + 1 < p.NC) {
-      El.load(elem + (c * Elem<R>::len) * B + b, B);
+      if (c + 2 < p.NC) Nx.load(erow + (c + 1) * Elem<R>::len, 1);
       ok = compose_state<R>(m, P, El) && ok;
+      El = Nx;
     }
   }
   if (!ok) flag(a.status, b, EKS_STATUS_SCAN);
@@ -510,7 +517,7 @@ __global__ __launch_bounds__(64) void k_c2_fscan_w(SmoothArgs a, ChunkPlan p) {
   agg.set_identity();
   for (long long c = c0; c < c1; ++c) {
     Elem<R> e;
-    e.load(elem + (c * Elem<R>::len) * B + b, B);
+    e.load(elem + (b * NC + c) * Elem<R>::len, 1);
     Elem<R> t;
     ok = compose_elem<R>(agg, e, t) && ok;
     agg = t;
@@ -535,7 +542,7 @@ __global__ __launch_bounds__(64) void k_c2_fscan_w(SmoothArgs a, ChunkPlan p) {
       load_mat<R, R>(pp + L::S0, P);
       store_state<R>(cst + b, B, m, P);  // chunk 0 starts from the prior
       Elem<R> e0;
-      e0.load(elem + b, B);
+      e0.load(elem + b * NC * Elem<R>::len, 1);
 #pragma unroll
       for (int i = 0; i < R; ++i) {
         m[i] = e0.bb[i];
@@ -555,7 +562,7 @@ __global__ __launch_bounds__(64) void k_c2_fscan_w(SmoothArgs a, ChunkPlan p) {
       store_state<R>(cst + (c * KS) * B + b, B, m, P);
       if (c + 1 < c1) {
         Elem<R> e;
-        e.load(elem + (c * Elem<R>::len) * B + b, B);
+        e.load(elem + (b * NC + c) * Elem<R>::len, 1);
         ok = compose_state<R>(m, P, e) && ok;
       }
     }
@@ -614,12 +621,12 @@ __global__ __launch_bounds__(64) void k_c4_bscan_w(SmoothArgs a, ChunkPlan p) {
   const long long c0 = min(NC, (long long)l * q), c1 = min(NC, c0 + q);
   auto load_map = [&](long long c) {
     Affine<R> f;
-    const double *s = bw + (c * (R * R + R)) * B + b;
+    const double *s = bw + (b * NC + c) * (R * R + R);
 #pragma unroll
     for (int i = 0; i < R; ++i) {
-      f.g[i] = s[(R * R + i) * B];
+      f.g[i] = s[R * R + i];
 #pragma unroll
-      for (int j = 0; j < R; ++j) f.G[i][j] = s[(i * R + j) * B];
+      for (int j = 0; j < R; ++j) f.G[i][j] = s[i * R + j];
     }
     return f;
   };
@@ -753,13 +760,14 @@ __global__ __launch_bounds__(kBlock) void k_c3_rerun(SmoothArgs a, ChunkPlan p) 
       }
     }
   }
-  double *bw = (double *)(a.ws + p.bwd_off);
+  // chunk maps are stored trajectory-major: row (b, c) = [G (R*R) | g (R)]
+  double *bw = (double *)(a.ws + p.bwd_off) + ((long long)b * p.NC + c) * (R * R + R);
 #pragma unroll
   for (int i = 0; i < R; ++i)
 #pragma unroll
-    for (int j = 0; j < R; ++j) pl(bw, c * (R * R + R) + i * R + j, B, b) = G[i][j];
+    for (int j = 0; j < R; ++j) bw[i * R + j] = G[i][j];
 #pragma unroll
-  for (int i = 0; i < R; ++i) pl(bw, c * (R * R + R) + R * R + i, B, b) = g[i];
+  for (int i = 0; i < R; ++i) bw[R * R + i] = g[i];
   pl((double *)(a.ws + p.nllp_off), c, B, b) = acc.value((double)(e - s) * N);
   if (!ok) flag(a.status, b, EKS_STATUS_SINGULAR);
 }
@@ -771,28 +779,43 @@ __global__ __launch_bounds__(64) void k_c4_bscan(SmoothArgs a, ChunkPlan p) {
   if (b >= B) return;
   const double *bw = (const double *)(a.ws + p.bwd_off);
   double *msend = (double *)(a.ws + p.msend_off);
-  double ms[R];
+  const double *np_ = (const double *)(a.ws + p.nllp_off);
+  auto load_map = [&](long long c, double (&G)[R][R], double (&g)[R]) {
+    const double *q = bw + (b * p.NC + c) * (R * R + R);
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      g[i] = q[R * R + i];
+#pragma unroll
+      for (int j = 0; j < R; ++j) G[i][j] = q[i * R + j];
+    }
+  };
+  double ms[R], G[R][R], g[R], Gn[R][R], gn[R];
 #pragma unroll
   for (int i = 0; i < R; ++i) ms[i] = 0.0;
+  load_map(p.NC - 1, G, g);
   for (long long c = p.NC - 1; c >= 0; --c) {
-    const double *q = bw + (c * (R * R + R)) * B + b;
+    if (c >= 1) load_map(c - 1, Gn, gn);  // next map in flight during this one
     double nx[R];
 #pragma unroll
     for (int i = 0; i < R; ++i) {
-      double s = q[(R * R + i) * B];
+      double s = g[i];
 #pragma unroll
-      for (int j = 0; j < R; ++j) s = fma(q[(i * R + j) * B], ms[j], s);
+      for (int j = 0; j < R; ++j) s = fma(G[i][j], ms[j], s);
       nx[i] = s;
     }
 #pragma unroll
     for (int i = 0; i < R; ++i) ms[i] = nx[i];
     if (c >= 1) {
 #pragma unroll
-      for (int i = 0; i < R; ++i) msend[((c - 1) * R + i) * B + b] = ms[i];
+      for (int i = 0; i < R; ++i) {
+        msend[((c - 1) * R + i) * B + b] = ms[i];
+        g[i] = gn[i];
+#pragma unroll
+        for (int j = 0; j < R; ++j) G[i][j] = Gn[i][j];
+      }
     }
   }
   if (a.nll) {
-    const double *np_ = (const double *)(a.ws + p.nllp_off);
     double s = 0.0;
     for (long long c = 0; c < p.NC; ++c) s += np_[c * B + b];
     a.nll[b] = s;
