@@ -1,31 +1,35 @@
 #!/usr/bin/env python3
 """Throughput benchmark of the fused EKS hot path on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 4]
     torchrun --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
-Workload (BASELINE.json configs[3], "config 4"): a batch of 1024 videos x 17
-keypoints, 5 ensemble members, 10 000 frames, single-view EKS -- 17 408
-independent keypoint trajectories, 1.74e8 keypoint-timesteps per pass.  The
-batch is fixed and sharded over the N ranks by video (strong scaling); at
-N = 1 one GPU smooths all of it (7 GB of float32 member predictions).
+Default workload (BASELINE.json configs[3], "config 4"): a batch of 1024
+videos x 17 keypoints, 5 ensemble members, 10 000 frames, single-view EKS --
+17 408 independent keypoint trajectories, 1.74e8 keypoint-timesteps per
+pass.  The batch is fixed and sharded over the N ranks by video (strong
+scaling, no data-path collective); at N = 1 one GPU smooths all of it (7 GB
+of float32 member predictions).  --config 2 / 3 / 5 run the other GPU
+configurations of BASELINE.json (one keypoint set per rank: replicas).
 
-A step = one pass of the hot path over the rank's shard, inputs resident in
-HBM: ensemble median/variance over the 5 members -> forward Kalman filter ->
-RTS backward pass -> projection + offsets, float64 recursions, smoothed
-(x, y) float64 written to HBM (eks_smooth, include/eks_hip.h).  The model of
-each trajectory (offsets, S0, Q from the low-variance
-frames) is fitted once before timing (eks_amd.fit.singleview_model_batch)
-and is not part of the step.
+A step = one pass of the hot path over the rank's trajectories, inputs
+resident in HBM: ensemble median/variance over the members -> forward Kalman
+filter -> RTS backward pass -> projection + offsets, float64 recursions,
+smoothed coordinates (float64) written to HBM (eks_smooth in
+include/eks_hip.h).  Config 5's step also scores an 8x8 grid of
+(diameter_s, com_s) pupil models by their innovation NLL (one filter-only
+batched call) before smoothing the best one.  Per-trajectory models (offsets,
+S0, Q: SURVEY.md §8 A6-A8) are fitted once before timing.
 
-Synthetic data: per video a seeded (4 + video index)
-Gaussian random walk per keypoint (sigma 2 px, start U(50, 450)), member
-noise sigma_e ~ U(0.5, 3) px, 1 % outliers of 30 px; values float32.
+Synthetic data: seeded random walks / AR(1) latents, member
+noise sigma_e ~ U(0.5, 3) px, 1 % outliers of 30 px (single/multi-view);
+values float32.
 
-Prints ONE JSON line (rank 0) with the throughput, the roofline of the
-dominant kernel (HIP events on the launch stream) and the CPU baseline
-(the numpy oracle on a bounded sample, 1 core).
+Prints ONE JSON line (rank 0): throughput, the roofline of the smoother's
+kernels (HIP events recorded by libeks_hip on the launch stream), the CPU
+baseline (the numpy oracle on a bounded sample, 1 core) and max|d| between
+the GPU and CPU outputs on that sample.
 """
 from __future__ import annotations
 
@@ -48,28 +52,37 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--videos", type=int, default=1024)
+    ap.add_argument("--config", type=int, default=4, choices=[2, 3, 4, 5],
+                    help="BASELINE.json configuration (1-based index)")
+    ap.add_argument("--videos", type=int, default=1024, help="config 4: videos in the batch")
     ap.add_argument("--keypoints", type=int, default=17)
     ap.add_argument("--members", type=int, default=5)
-    ap.add_argument("--frames", type=int, default=10000)
+    ap.add_argument("--frames", type=int, default=None,
+                    help="frames per video (default: 10k / 100k / 50k / 1M for configs 4/2/3/5)")
     ap.add_argument("--smooth-param", type=float, default=0.01)
     ap.add_argument("--quantile-keep", type=float, default=25.0)
-    ap.add_argument("--seed", type=int, default=4)
+    ap.add_argument("--seed", type=int, default=None)
     ap.add_argument("--algo", type=int, default=0, help="eks_smooth algo (0 auto)")
-    ap.add_argument("--cpu-sample", type=int, default=24,
-                    help="trajectories of the workload timed on the CPU oracle (rank 0, N=1)")
+    ap.add_argument("--cpu-sample", type=int, default=None,
+                    help="trajectories timed on the CPU oracle (rank 0, N=1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--gather", action="store_true",
-                    help="after timing, gather all outputs to rank 0 once (RCCL) and report it")
+                    help="config 4: after timing, gather all outputs to rank 0 (RCCL) once")
     ap.add_argument("--scaling", choices=["strong", "weak"], default="strong",
-                    help="strong: the video batch is split over ranks; weak: every rank "
-                         "smooths --videos videos")
-    return ap.parse_args()
+                    help="config 4: strong = the video batch is split over ranks; weak = "
+                         "every rank smooths --videos videos")
+    a = ap.parse_args()
+    a.frames = a.frames or {4: 10000, 2: 100000, 3: 50000, 5: 1000000}[a.config]
+    a.seed = a.config if a.seed is None else a.seed
+    return a
 
 
+# ---------------------------------------------------------------------------
+# synthetic data
+# ---------------------------------------------------------------------------
 def gen_videos(torch, videos, K, E, T, seed0, device):
-    """(T, E, 2, B) float32 member predictions for the given video ids,
-    trajectory index b = video_local * K + keypoint (innermost axis)."""
+    """(T, E, 2, B) float32 single-view member predictions for the given video
+    ids (seed seed0 + video id), trajectory b = video_local * K + keypoint."""
     B = len(videos) * K
     obs = torch.empty((T, E, 2, B), dtype=torch.float32, device=device)
     for i, v in enumerate(videos):
@@ -90,21 +103,27 @@ def gen_videos(torch, videos, K, E, T, seed0, device):
     return obs
 
 
-def fit_models(torch, lib_mod, obs_view, s, q, chunk=2048):
-    """Per-trajectory single-view models, fitted on device in chunks."""
-    from eks_amd import _lib, batch, fit
+def ensemble_dev(torch, obs_view, mode="median"):
+    """(B, T, n) preds / vars of a (B, T, E, n) member view (eks_ensemble)."""
+    from eks_amd import _lib
     B, T, E, n = obs_view.shape
-    lib = _lib.load()
+    preds = torch.empty((B, T, n), dtype=torch.float64, device=obs_view.device)
+    var = torch.empty_like(preds)
+    sb, st, se, sj = obs_view.stride()
+    dt = _lib.EKS_F32 if obs_view.dtype == torch.float32 else _lib.EKS_F64
+    _lib.check(_lib.load().eks_ensemble(obs_view.data_ptr(), dt, B, T, E, n, sb, st, se, sj,
+                                        _lib.EKS_MEDIAN if mode == "median" else _lib.EKS_MEAN,
+                                        preds.data_ptr(), var.data_ptr(), _lib.stream_ptr()),
+               "eks_ensemble")
+    return preds, var
+
+
+def fit_singleview(torch, obs_view, s, q, chunk=2048):
+    """Per-trajectory single-view models, fitted on device in chunks."""
+    from eks_amd import batch, fit
     parts = []
-    for lo in range(0, B, chunk):
-        hi = min(B, lo + chunk)
-        sub = obs_view[lo:hi]
-        preds = torch.empty((hi - lo, T, n), dtype=torch.float64, device=obs_view.device)
-        var = torch.empty_like(preds)
-        sb, st, se, sj = sub.stride()
-        _lib.check(lib.eks_ensemble(sub.data_ptr(), _lib.EKS_F32, hi - lo, T, E, n, sb, st, se,
-                                    sj, _lib.EKS_MEDIAN, preds.data_ptr(), var.data_ptr(),
-                                    _lib.stream_ptr()), "eks_ensemble")
+    for lo in range(0, obs_view.shape[0], chunk):
+        preds, var = ensemble_dev(torch, obs_view[lo:lo + chunk])
         m = fit.singleview_model_batch(preds, var, s, q)
         parts.append(batch.pack_params(m["m0"], m["S0"], m["A"], m["Q"], m["C"], m["offset"],
                                        device=obs_view.device))
@@ -112,30 +131,170 @@ def fit_models(torch, lib_mod, obs_view, s, q, chunk=2048):
     return torch.cat(parts, dim=0).contiguous()
 
 
-def cpu_baseline(torch, obs_tm, out_view, n_traj, T, s, q):
-    """Time the numpy oracle (the reference's algorithm, 1 core) on the first
-    n_traj trajectories of the workload; compare with the GPU outputs."""
+# ---------------------------------------------------------------------------
+# workloads: each returns a dict with step(), units, bytes_per_unit, cpu()
+# ---------------------------------------------------------------------------
+def workload_singleview(torch, a, dev, rank, world, config):
+    from eks_amd import _lib, batch, dist
+    K, E, T = a.keypoints, a.members, a.frames
+    if config == 4:
+        if a.scaling == "strong":
+            lo, hi = dist.shard_range(a.videos, world, rank)
+        else:
+            lo, hi = rank * a.videos, (rank + 1) * a.videos
+        videos = range(lo, hi)
+    else:  # config 2: one video of K keypoints per rank (replicas)
+        videos = range(0, 1)
+    B = len(videos) * K
+    obs_tm = gen_videos(torch, videos, K, E, T, a.seed, dev)          # (T, E, 2, B)
+    obs = obs_tm.permute(3, 0, 1, 2)                                   # (B, T, E, 2) view
+    params = fit_singleview(torch, obs, a.smooth_param, a.quantile_keep)
+    out = torch.empty((T, B, 2), dtype=torch.float64, device=dev).permute(1, 0, 2)
+    status = torch.empty((B,), dtype=torch.int32, device=dev)
+    flags = _lib.EKS_MODEL_A_IDENTITY | _lib.EKS_MODEL_C_IDENTITY  # single-view: A = C = I2
+
+    def step():
+        batch.smooth(obs, params, n=2, r=2, out=out, status=status, algo=a.algo, flags=flags)
+
+    def cpu(n_traj):
+        import numpy as np
+        from oracle import eks_oracle as O
+        host = obs_tm[:, :, :, :n_traj].cpu().numpy().astype(np.float64)  # (T, E, 2, b)
+        gpu = out[:n_traj].cpu().numpy()
+        t0 = time.perf_counter()
+        outs = [O.singleview_smooth(np.ascontiguousarray(np.transpose(host[..., b], (1, 0, 2))),
+                                    a.smooth_param, a.quantile_keep)[0] for b in range(n_traj)]
+        dt = time.perf_counter() - t0
+        diff = max(float(np.abs(o - gpu[b]).max()) for b, o in enumerate(outs))
+        return n_traj * T / dt, dt, diff, (f"{n_traj} trajectories x {T} frames of this workload "
+                                           f"(oracle.singleview_smooth: ensemble + fit + filter + "
+                                           f"smoother, numpy, 1 thread)")
+
+    desc = (f"config {config}: " + (f"batch of {a.videos} videos x " if config == 4 else "1 video x ")
+            + f"{K} keypoints x {E} members x {T} frames, single-view EKS (ensemble median/var "
+            f"-> forward KF -> RTS -> projection), float32 members, float64 recursions/outputs")
+    return dict(step=step, status=status, units=B * T, bytes_per_unit=E * 2 * 4 + 2 * 8,
+                cpu=cpu, cpu_default=24 if config == 4 else 2, desc=desc,
+                cfg=dict(videos=a.videos if config == 4 else 1, keypoints=K, members=E, frames=T,
+                         trajectories_per_rank=B, smooth_param=a.smooth_param,
+                         quantile_keep=a.quantile_keep),
+                key=f"config{config}-singleview-v{len(videos) * world if config == 4 else 1}"
+                    f"-k{K}-e{E}-t{T}-n{world}-{a.scaling}",
+                out=out, videos=videos)
+
+
+def workload_multiview(torch, a, dev, rank, world):
+    """config 3: V = 4 cameras x 17 keypoints x 50k frames, PCA multiview."""
     import numpy as np
-    from threadpoolctl import threadpool_limits
-    from oracle import eks_oracle as O
-    idx = list(range(n_traj))
-    host = obs_tm[:, :, :, :n_traj].cpu().numpy().astype(np.float64)  # (T, E, 2, b)
-    gpu = out_view[:n_traj].cpu().numpy()
-    maxdiff = 0.0
-    with threadpool_limits(1):
+    from eks_amd import _lib, batch, fit, synthetic
+    K, E, T, V = a.keypoints, a.members, a.frames, 4
+    rng = np.random.default_rng(a.seed)
+    st = synthetic.multiview_obs(rng, V, E, T, K=K)                   # (E, T, K, 8) f32
+    n = 2 * V
+    obs_tm = torch.from_numpy(np.ascontiguousarray(st.transpose(1, 0, 3, 2))).to(dev)  # (T,E,8,K)
+    obs = obs_tm.permute(3, 0, 1, 2)
+    preds, var = ensemble_dev(torch, obs)
+    preds, var = preds.cpu().numpy(), var.cpu().numpy()
+    models = [fit.multicam_model(preds[k], var[k], a.smooth_param, a.quantile_keep)
+              for k in range(K)]
+    stackp = lambda key: np.stack([m[key] for m in models])  # noqa: E731
+    params = batch.pack_params(stackp("m0"), stackp("S0"), stackp("A"), stackp("Q"), stackp("C"),
+                               stackp("offset"), device=dev)
+    flags = batch.model_flags(stackp("A"), stackp("C"))
+    out = torch.empty((T, K, n), dtype=torch.float64, device=dev).permute(1, 0, 2)
+    status = torch.empty((K,), dtype=torch.int32, device=dev)
+
+    def step():
+        batch.smooth(obs, params, n=n, r=3, out=out, status=status, algo=a.algo, flags=flags)
+
+    def cpu(n_traj):
+        from oracle import eks_oracle as O
+        gpu = out[:n_traj].cpu().numpy()
         t0 = time.perf_counter()
         outs = []
-        for b in idx:
-            st = np.ascontiguousarray(np.transpose(host[..., b], (1, 0, 2)))  # (E, T, 2)
-            out, _, _ = O.singleview_smooth(st, s, q)
-            outs.append(out)
+        for k in range(n_traj):
+            cams = [st[:, :, k, 2 * c:2 * c + 2].astype(np.float64) for c in range(V)]
+            outs.append(O.multicam_smooth(cams, a.smooth_param, a.quantile_keep)[0])
         dt = time.perf_counter() - t0
-    for b, out in zip(idx, outs):
-        maxdiff = max(maxdiff, float(np.abs(out - gpu[b]).max()))
-    return dict(value=n_traj * T / dt, unit="kp-ts/s", cores=1, kind="port",
-                sample=f"{n_traj} trajectories x {T} frames of this workload "
-                       f"(oracle/eks_oracle.singleview_smooth: ensemble + fit + filter + "
-                       f"smoother, numpy 1 thread), {dt:.1f} s"), maxdiff
+        diff = max(float(np.abs(o - gpu[k]).max()) for k, o in enumerate(outs))
+        return n_traj * T / dt, dt, diff, (f"{n_traj} keypoints x {T} frames x {V} cameras of "
+                                           f"this workload (oracle.multicam_smooth, numpy, "
+                                           f"1 thread)")
+
+    desc = (f"config 3: multiview PCA smoother, {V} cameras x {K} keypoints x {E} members x "
+            f"{T} frames (r=3 latent, n=8), float32 members, float64 recursions/outputs")
+    return dict(step=step, status=status, units=K * T, bytes_per_unit=E * n * 4 + n * 8,
+                cpu=cpu, cpu_default=2, desc=desc,
+                cfg=dict(cameras=V, keypoints=K, members=E, frames=T,
+                         smooth_param=a.smooth_param, quantile_keep=a.quantile_keep),
+                key=f"config3-multiview-k{K}-e{E}-t{T}-n{world}")
+
+
+def workload_pupil(torch, a, dev, rank, world):
+    """config 5: IBL pupil, 1M frames x 4 keypoints, NLL sweep + smooth."""
+    import numpy as np
+    from eks_amd import batch, fit, synthetic
+    E, T = a.members, a.frames
+    st = synthetic.pupil_obs(np.random.default_rng(a.seed), E, T, a=0.99)  # (E, T, 8) f32
+    obs_tm = torch.from_numpy(np.ascontiguousarray(st.transpose(1, 0, 2))).to(dev)  # (T, E, 8)
+    obs = obs_tm.unsqueeze(0)                                          # (1, T, E, 8) view
+    preds, _ = ensemble_dev(torch, obs)
+    preds = preds[0].cpu().numpy()
+    d_grid = 1.0 - np.geomspace(1e-4, 1e-1, 8)
+    c_grid = 1.0 - np.geomspace(1e-4, 1e-1, 8)
+    base = fit.pupil_model(preds, np.diag([0.99, 0.99, 0.99]))
+    var0 = np.diag(base["S0"])
+    cands = []
+    for d in d_grid:
+        for c in c_grid:
+            A = np.diag([d, c, c])
+            cands.append(dict(base, A=A, Q=np.diag(var0 * (1 - np.diag(A) ** 2))))
+    stackp = lambda key: np.stack([m[key] for m in cands])  # noqa: E731
+    params = batch.pack_params(stackp("m0"), stackp("S0"), stackp("A"), stackp("Q"), stackp("C"),
+                               stackp("offset"), device=dev)
+    out = torch.empty((T, 1, 8), dtype=torch.float64, device=dev).permute(1, 0, 2)
+    ms = torch.empty((1, T, 3), dtype=torch.float64, device=dev)
+    status = torch.empty((1,), dtype=torch.int32, device=dev)
+    cands_obs = obs.expand(len(cands), -1, -1, -1)  # batch stride 0: members shared
+    state = {}
+
+    def step():
+        scores = batch.nll(cands_obs, params, n=8, r=3, algo=a.algo, check=False)
+        best = torch.argmin(scores)                                    # stays on device
+        p_best = params.index_select(0, best.view(1)).contiguous()
+        r = batch.smooth(obs, p_best, n=8, r=3, out=out, want_ms=True, status=status,
+                         algo=a.algo)
+        state["best"], state["scores"], state["ms"] = best, scores, r["ms"]
+
+    def cpu(_n):
+        from oracle import eks_oracle as O
+        Tc = min(T, 200000)  # bounded sample: the first Tc frames, chosen model
+        b = int(state["best"].item())
+        Ab = cands[b]["A"]
+        t0 = time.perf_counter()
+        mk, _, _, _ = O.pupil_smooth(st[:, :Tc].astype(np.float64), Ab)
+        dt = time.perf_counter() - t0
+        # the GPU reference for the same prefix and model
+        sub = obs[:, :Tc]
+        from eks_amd import fit as F
+        pre = F.pupil_model(O.ensemble_array(st[:, :Tc].astype(np.float64))[0], Ab)
+        pb = batch.pack_params(pre["m0"], pre["S0"], pre["A"], pre["Q"], pre["C"], pre["offset"],
+                               device=dev)
+        g = batch.smooth(sub, pb, n=8, r=3)["out"][0].cpu().numpy()
+        diff = float(np.abs(g - mk).max())
+        return 4 * Tc / dt, dt, diff, (f"first {Tc} frames x 4 keypoints, best model "
+                                       f"(oracle.pupil_smooth, numpy, 1 thread); the GPU step "
+                                       f"also scores {len(cands)} candidate models")
+
+    desc = (f"config 5: IBL-pupil smoother, {T} frames x 4 keypoints x {E} members (r=3 latent, "
+            f"n=8): NLL sweep over {len(cands)} (diameter_s, com_s) models (filter-only, "
+            f"batched) + smoothing of the argmin, float64")
+    return dict(step=step, status=status, units=4 * T, bytes_per_unit=(32 * E + 88) / 4,
+                cpu=cpu, cpu_default=1, desc=desc,
+                cfg=dict(frames=T, keypoints=4, members=E, candidates=len(cands)),
+                key=f"config5-pupil-t{T}-n{world}", extra=lambda: dict(
+                    sweep_candidates=len(cands),
+                    best_model=[float(x) for x in np.diag(cands[int(state['best'])]['A'])]))
 
 
 def load_pmc(workload_key):
@@ -146,15 +305,14 @@ def load_pmc(workload_key):
         d = json.load(open(path))
     except Exception:
         return None
-    if d.get("workload_key") != workload_key:
-        return None
-    return d
+    return d if d.get("workload_key") == workload_key else None
 
 
 def main():
     a = parse()
     import torch
-    from eks_amd import _lib, batch, dist
+    from eks_amd import _lib, dist
+    from threadpoolctl import threadpool_limits
     rank, world, local = dist.init()
     if world != a.gpus and rank == 0:
         print(f"[bench] note: --gpus {a.gpus} but WORLD_SIZE={world}; using {world}",
@@ -162,76 +320,73 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     _lib.require_gpu()
-    K, E, T = a.keypoints, a.members, a.frames
-    if a.scaling == "strong":
-        lo, hi = dist.shard_range(a.videos, world, rank)
-    else:
-        lo, hi = rank * a.videos, (rank + 1) * a.videos
-    videos = range(lo, hi)
-    B = len(videos) * K
     t_setup = time.perf_counter()
-    obs_tm = gen_videos(torch, videos, K, E, T, a.seed, dev)          # (T, E, 2, B)
-    obs = obs_tm.permute(3, 0, 1, 2)                                   # (B, T, E, 2) view
-    params = fit_models(torch, _lib, obs, a.smooth_param, a.quantile_keep)
-    out = torch.empty((T, B, 2), dtype=torch.float64, device=dev).permute(1, 0, 2)
-    status = torch.empty((B,), dtype=torch.int32, device=dev)
+    if a.config in (2, 4):
+        w = workload_singleview(torch, a, dev, rank, world, a.config)
+    elif a.config == 3:
+        w = workload_multiview(torch, a, dev, rank, world)
+    else:
+        w = workload_pupil(torch, a, dev, rank, world)
     torch.cuda.synchronize()
     setup_s = time.perf_counter() - t_setup
-
-    flags = _lib.EKS_MODEL_A_IDENTITY | _lib.EKS_MODEL_C_IDENTITY  # single-view: A = C = I2
-
-    def step():
-        batch.smooth(obs, params, n=2, r=2, out=out, status=status, algo=a.algo, flags=flags)
+    step = w["step"]
 
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
-    if int((status != 0).sum().item()) != 0:
-        raise RuntimeError("singular trajectories in the bench workload")
+    if int((w["status"] != 0).sum().item()) != 0:
+        raise RuntimeError("singular / mis-flagged trajectories in the bench workload")
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k in range(a.steps):
+    for _ in range(a.steps):
         step()
     torch.cuda.synchronize()
     dist.barrier()
     elapsed = time.perf_counter() - t0
     elapsed_max = dist.max_over_ranks(elapsed, device=dev)
     # per-kernel launch durations: HIP events recorded by libeks_hip on the
-    # launch stream between the kernels of each eks_smooth call (separate pass
+    # launch stream around each kernel of each eks_smooth call (separate pass,
     # so the events do not perturb the timed loop above)
-    _lib.profile_begin(a.steps)
-    for k in range(a.steps):
+    _lib.profile_begin(4 * a.steps)
+    for _ in range(a.steps):
         step()
     kernels = _lib.profile_end()
-    kern_ms = sum(ms for _, ms in kernels)
+    calls_per_step = 2 if a.config == 5 else 1
+    kern_ms = sum(ms for _, ms in kernels) * calls_per_step
     kern_ms_max = dist.max_over_ranks(kern_ms, device=dev)
-    units_local = B * T
+    units_local = w["units"]
     units_total = dist.sum_over_ranks(units_local, device=dev)
 
     gather_ms = None
-    if a.gather and world > 1:
+    if a.gather and world > 1 and a.config == 4:
         torch.cuda.synchronize()
         dist.barrier()
         g0 = time.perf_counter()
-        local = out.permute(1, 0, 2).reshape(T, len(videos), K, 2).permute(1, 0, 2, 3)
-        full = dist.gather_to_rank0(local.contiguous(), a.videos)
+        T, K = a.frames, a.keypoints
+        nv = len(w["videos"])
+        loc = w["out"].permute(1, 0, 2).reshape(T, nv, K, 2).permute(1, 0, 2, 3).contiguous()
+        full = dist.gather_to_rank0(loc, a.videos)
         torch.cuda.synchronize()
         gather_ms = (time.perf_counter() - g0) * 1e3
         del full
 
     cpu = None
     maxdiff = None
-    if rank == 0 and world == 1 and not a.no_cpu_baseline and a.cpu_sample > 0:
-        cpu, maxdiff = cpu_baseline(torch, obs_tm, out, min(a.cpu_sample, B), T,
-                                    a.smooth_param, a.quantile_keep)
+    n_cpu = w["cpu_default"] if a.cpu_sample is None else a.cpu_sample
+    if rank == 0 and world == 1 and not a.no_cpu_baseline and n_cpu > 0:
+        with threadpool_limits(1):
+            v, dt, maxdiff, sample = w["cpu"](n_cpu)
+        cpu = dict(value=v, unit="kp-ts/s", cores=1, kind="port",
+                   sample=f"{sample}, {dt:.1f} s")
 
     if rank == 0:
         value = units_total / elapsed_max * a.steps
-        bytes_per_unit = E * 2 * 4 + 2 * 8  # f32 members in, f64 (x, y) out
-        achieved = bytes_per_unit * units_local / (kern_ms_max * 1e-3) / 1e9
-        wk = f"config4-singleview-v{a.videos}-k{K}-e{E}-t{T}-n{world}-{a.scaling}"
-        pmc = load_pmc(wk)
+        achieved = w["bytes_per_unit"] * units_local / (kern_ms_max * 1e-3) / 1e9
+        pmc = load_pmc(w["key"])
+        scaling = "strong" if (a.config == 4 and a.scaling == "strong") else "weak"
+        par = (f"videos sharded over {world} rank(s), no data-path collective" if a.config == 4
+               else f"{world} independent replica(s)")
         line = {
             "metric": METRIC,
             "value": value,
@@ -241,21 +396,11 @@ def main():
             "warmup": a.warmup,
             "ms_per_step": elapsed_max / a.steps * 1e3,
             "higher_is_better": True,
-            "scaling": a.scaling,
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic",
-            "config": {
-                "workload": f"config 4: batch of {a.videos} videos x {K} keypoints x {E} "
-                            f"members x {T} frames, single-view EKS (ensemble median/var -> "
-                            f"forward KF -> RTS -> projection), float32 members, float64 "
-                            f"recursions/outputs, {'split over' if a.scaling == 'strong' else 'per'} "
-                            f"{world} GPU(s)",
-                "videos": a.videos, "keypoints": K, "members": E, "frames": T,
-                "trajectories_per_rank": B, "smooth_param": a.smooth_param,
-                "quantile_keep": a.quantile_keep, "algo": a.algo,
-                "parallelism": f"videos sharded over {world} rank(s), no data-path collective",
-            },
+            "config": dict(workload=w["desc"], algo=a.algo, parallelism=par, **w["cfg"]),
             "roofline": {
                 "bound": "hbm",
                 "achieved": achieved,
@@ -266,13 +411,15 @@ def main():
                 "kernel": "eks_smooth (" + " + ".join(n for n, _ in kernels) + ")",
                 "kernel_ms": kern_ms_max,
                 "kernels_ms": {n: round(ms, 4) for n, ms in kernels},
-                "bytes_per_unit": bytes_per_unit,
+                "bytes_per_unit": w["bytes_per_unit"],
                 "units_per_launch": units_local,
             },
             "cpu_baseline": cpu,
             "max_abs_diff_vs_cpu": maxdiff,
             "setup_s": round(setup_s, 2),
         }
+        if "extra" in w:
+            line.update(w["extra"]())
         if gather_ms is not None:
             line["gather_ms"] = gather_ms
         print(json.dumps(line))

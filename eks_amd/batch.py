@@ -77,7 +77,7 @@ def model_flags(A, C) -> int:
 
 def smooth(obs, params, *, n: int, r: int, mode: str = "median", out=None, want_ms=False,
            want_nll=False, status=None, algo: int = 0, flags: int = 0, stream=None,
-           check: bool = False):
+           check: bool = False, want_out: bool = True):
     """Fused ensemble -> forward -> backward -> projection for B trajectories.
 
     Returns dict(out=(B,T,n) view, ms=(B,T,r) or None, nll=(B,) or None,
@@ -107,7 +107,9 @@ def smooth(obs, params, *, n: int, r: int, mode: str = "median", out=None, want_
             or not params.is_contiguous():
         raise ValueError(f"params must be a contiguous ({B}, {param_len(n, r)}) float64 tensor")
     dev = obs.device
-    if out is None:
+    if not want_out:  # filter only: NLL per trajectory, no backward pass
+        want_nll, want_ms, out = True, False, None
+    elif out is None:
         out = torch.empty((T, B, n), dtype=torch.float64, device=dev).permute(1, 0, 2)
     ms = torch.empty((B, T, r), dtype=torch.float64, device=dev) if want_ms else None
     nll = torch.empty((B,), dtype=torch.float64, device=dev) if want_nll else None
@@ -117,11 +119,12 @@ def smooth(obs, params, *, n: int, r: int, mode: str = "median", out=None, want_
     nbytes = lib.eks_smooth_workspace_bytes(B, T, n, r, E, algo)
     ws = workspace(nbytes, dev)
     sb, st, se, sj = obs.stride()
-    ob, ot, oj = out.stride()
+    ob, ot, oj = out.stride() if out is not None else (0, 0, 0)
     _lib.check(lib.eks_smooth(
         obs.data_ptr(), dt, B, T, E, n, r, sb, st, se, sj,
         _lib.EKS_MEDIAN if mode == "median" else _lib.EKS_MEAN, params.data_ptr(),
-        out.data_ptr(), ob, ot, oj, ms.data_ptr() if ms is not None else None,
+        out.data_ptr() if out is not None else None, ob, ot, oj,
+        ms.data_ptr() if ms is not None else None,
         nll.data_ptr() if nll is not None else None, ws.data_ptr(), ws.numel(), flags, algo,
         status.data_ptr(), _lib.stream_ptr(stream)), "eks_smooth")
     res = dict(out=out, ms=ms, nll=nll, status=status)
@@ -132,10 +135,21 @@ def smooth(obs, params, *, n: int, r: int, mode: str = "median", out=None, want_
         if st_all & _lib.EKS_STATUS_SCAN and algo != 1:
             return smooth(obs, params, n=n, r=r, mode=mode, out=out, want_ms=want_ms,
                           want_nll=want_nll, status=status, algo=1, flags=flags,
-                          stream=stream, check=True)
+                          stream=stream, check=True, want_out=want_out)
         if st_all & _lib.EKS_STATUS_SINGULAR:
             raise np.linalg.LinAlgError("Singular matrix")
     return res
+
+
+def nll(obs, params, *, n: int, r: int, mode: str = "median", flags: int = 0, algo: int = 0,
+        check: bool = True):
+    """Filter-only pass: the innovation NLL of every
+    trajectory / candidate model, no backward pass.  To score C candidate
+    models of ONE trajectory, pass ``obs.expand(C, -1, -1, -1)`` (batch
+    stride 0: the members are read once per candidate from the same memory)
+    and C rows of params."""
+    return smooth(obs, params, n=n, r=r, mode=mode, flags=flags, algo=algo, check=check,
+                  want_out=False)["nll"]
 
 
 def status_bits(status) -> int:

@@ -44,7 +44,9 @@ int eks_smooth(const void *obs, int obs_dtype, int64_t B, int64_t T, int E, int 
                double *out, int64_t ob, int64_t ot, int64_t oj, double *ms, double *nll,
                void *workspace, size_t workspace_bytes, int model_flags, int algo,
                int32_t *status, void *stream) {
-  if (!obs || !params || !out || !status) return set_err(EKS_ERR_ARG, "eks_smooth: NULL pointer");
+  if (!obs || !params || !status) return set_err(EKS_ERR_ARG, "eks_smooth: NULL pointer");
+  if (!out && (!nll || ms))
+    return set_err(EKS_ERR_ARG, "eks_smooth: out may be NULL only for a filter-only (nll) call");
   if (B < 0 || T < 1 || E < 1) return set_err(EKS_ERR_ARG, "eks_smooth: need B>=0, T>=1, E>=1");
   if (E > kMaxMembers) return set_err(EKS_ERR_UNSUPPORTED, "eks_smooth: E=%d > %d", E, kMaxMembers);
   if (mode != EKS_MEDIAN && mode != EKS_MEAN)

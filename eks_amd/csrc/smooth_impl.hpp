@@ -108,6 +108,7 @@ inline long long chunk_len(long long B, long long T, int r) {
 struct ChunkPlan {
   long long L = 0, NC = 0, NSUB = 0;
   int LS = 8;
+  int smooth = 1;  // 0: filter only (out == NULL): NLL, no backward pass
   size_t y_off = 0, ev_off = 0, elem_off = 0, cstart_off = 0, bwd_off = 0, nllp_off = 0,
          msend_off = 0, ckpt_off = 0, total = 0;
 };
@@ -268,6 +269,10 @@ __global__ __launch_bounds__(64) void k_smooth_seq(SmoothArgs a) {
     }
   }
   if (a.nll) a.nll[b] = acc.value((double)TT * N);
+  if (!a.out) {  // filter only
+    if (!ok) flag(a.status, b, EKS_STATUS_SINGULAR);
+    return;
+  }
   // backward
   double ms[R];
 #pragma unroll
@@ -715,7 +720,7 @@ __global__ __launch_bounds__(kBlock) void k_c3_rerun(SmoothArgs a, ChunkPlan p) 
     if (s + q < e) load_yev<N, YT>(ybuf, evbuf, s + q, B, b, yr[q], er[q]);
   long long k = 0;
   for (long long t0 = s; t0 < e; t0 += LS, ++k) {
-    store_state_pl<R>(ckpt, (c * p.NSUB + k) * KS, B, b, m, P);  // state before t0
+    if (p.smooth) store_state_pl<R>(ckpt, (c * p.NSUB + k) * KS, B, b, m, P);  // state before t0
 #pragma unroll
     for (int q = 0; q < LS; ++q) {
       const long long t = t0 + q;
@@ -729,6 +734,7 @@ __global__ __launch_bounds__(kBlock) void k_c3_rerun(SmoothArgs a, ChunkPlan p) 
         if (t + D < e) load_yev<N, YT>(ybuf, evbuf, t + D, B, b, yr[q % D], er[q % D]);
         if (t > 0) kf_predict<R, AI>(m, P, md.A, md.Q);
         kf_update<R, N, CI>(m, P, md.C, y, rv, acc, ok);
+        if (!p.smooth) continue;
         if (t + 1 < TT) {
           double J[R][R], d[R], GJ[R][R];
           ok = rts_gain<R, AI>(m, P, md.A, md.Q, J, d) && ok;
@@ -760,6 +766,9 @@ __global__ __launch_bounds__(kBlock) void k_c3_rerun(SmoothArgs a, ChunkPlan p) 
       }
     }
   }
+  pl((double *)(a.ws + p.nllp_off), c, B, b) = acc.value((double)(e - s) * N);
+  if (!ok) flag(a.status, b, EKS_STATUS_SINGULAR);
+  if (!p.smooth) return;
   // chunk maps are stored trajectory-major: row (b, c) = [G (R*R) | g (R)]
   double *bw = (double *)(a.ws + p.bwd_off) + ((long long)b * p.NC + c) * (R * R + R);
 #pragma unroll
@@ -768,8 +777,6 @@ __global__ __launch_bounds__(kBlock) void k_c3_rerun(SmoothArgs a, ChunkPlan p) 
     for (int j = 0; j < R; ++j) bw[i * R + j] = G[i][j];
 #pragma unroll
   for (int i = 0; i < R; ++i) bw[R * R + i] = g[i];
-  pl((double *)(a.ws + p.nllp_off), c, B, b) = acc.value((double)(e - s) * N);
-  if (!ok) flag(a.status, b, EKS_STATUS_SINGULAR);
 }
 
 template <int R>
@@ -820,6 +827,18 @@ __global__ __launch_bounds__(64) void k_c4_bscan(SmoothArgs a, ChunkPlan p) {
     for (long long c = 0; c < p.NC; ++c) s += np_[c * B + b];
     a.nll[b] = s;
   }
+}
+
+// filter-only calls (no `out`): the NLL of each trajectory is the sum of its
+// chunks' shares, in chunk order
+template <int R>
+__global__ __launch_bounds__(64) void k_c4_nll(SmoothArgs a, ChunkPlan p) {
+  const long long b = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (b >= a.B || !a.nll) return;
+  const double *np_ = (const double *)(a.ws + p.nllp_off);
+  double s = 0.0;
+  for (long long c = 0; c < p.NC; ++c) s += np_[c * a.B + b];
+  a.nll[b] = s;
 }
 
 template <int R, int N, typename YT, bool AI, bool CI, int LS>
@@ -936,7 +955,8 @@ int launch_shape(const SmoothArgs &a, int algo, long long L) {
     };
     return f32 ? go(float{}) : go(double{});
   }
-  const ChunkPlan p = make_plan(a.B, a.T, R, N, L);
+  ChunkPlan p = make_plan(a.B, a.T, R, N, L);
+  p.smooth = a.out != nullptr;
   const unsigned g256 = (unsigned)(p.NC * blocks_per_chunk(a.B));
   const unsigned g64 = grid_for(a.B, 64);
   // y is stored as float when it is exactly a member value (odd-E median of f32)
@@ -957,6 +977,12 @@ int launch_shape(const SmoothArgs &a, int algo, long long L) {
     hipLaunchKernelGGL((k_c3_rerun<R, N, YT, AI, CI, LS3>), dim3(g256), dim3(kBlock), 0, a.stream,
                        a, p);
     if (int rc = check_launch("k_c3_rerun")) return rc;
+    if (!p.smooth) {  // filter only: sum the NLL shares, no backward pass
+      prof_mark(a.stream, "k_c4_nll");
+      hipLaunchKernelGGL((k_c4_nll<R>), dim3(g64), dim3(64), 0, a.stream, a, p);
+      prof_call_end(a.stream);
+      return check_launch("k_c4_nll");
+    }
     prof_mark(a.stream, "k_c4_bscan");
     if (wave_scan)
       hipLaunchKernelGGL((k_c4_bscan_w<R>), dim3((unsigned)a.B), dim3(64), 0, a.stream, a, p);

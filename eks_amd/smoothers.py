@@ -88,6 +88,37 @@ def ensemble_kalman_smoother_pupil(markers_list, keypoint_names, tracker_name,
     return {'markers_df': markers_df, 'latents_df': pd.DataFrame(lat, columns=idx)}
 
 
+def pupil_smoothing_sweep(markers_list, keypoint_names, tracker_name, diameter_s_grid,
+                          com_s_grid):
+    """The pupil smoother with its smoothing parameters chosen by likelihood.
+
+    Every (diameter_s, com_s) pair of the grid defines a model
+    (A = diag(d, c, c), Q = var (1 - A^2): eks/pupil_smoother.py:140-147);
+    all candidates are scored in ONE filter-only batched call (the member
+    predictions are shared, batch stride 0) by their innovation NLL, and the
+    argmin is smoothed.  Returns ensemble_kalman_smoother_pupil's dict plus
+    'nll' (len(diameter_s_grid), len(com_s_grid)) and 'best' (d, c).
+    (The reference has no NLL loop: SURVEY.md §0; this is the build's.)"""
+    torch = _lib.require_gpu()
+    stack = np.stack([np.stack([np.asarray(df[k], dtype=np.float64) for k in fit.PUPIL_KEYS], 1)
+                      for df in markers_list])  # (E, T, 8)
+    E, T, n = stack.shape
+    preds, _ = core.ensemble_array(stack)
+    grid = [(d, c) for d in diameter_s_grid for c in com_s_grid]
+    models = [fit.pupil_model(preds, np.diag([d, c, c])) for d, c in grid]
+    stackp = lambda k: np.stack([m[k] for m in models])  # noqa: E731
+    params = batch.pack_params(stackp("m0"), stackp("S0"), stackp("A"), stackp("Q"),
+                               stackp("C"), stackp("offset"))
+    obs = torch.from_numpy(np.ascontiguousarray(stack)).to("cuda").permute(1, 0, 2).unsqueeze(0)
+    scores = batch.nll(obs.expand(len(grid), -1, -1, -1), params, n=n, r=3).cpu().numpy()
+    best = grid[int(np.argmin(scores))]
+    res = ensemble_kalman_smoother_pupil(markers_list, keypoint_names, tracker_name,
+                                         np.diag([best[0], best[1], best[1]]))
+    res["nll"] = scores.reshape(len(diameter_s_grid), len(com_s_grid))
+    res["best"] = best
+    return res
+
+
 def ensemble_kalman_smoother_single_view(markers_list, keypoint_ensemble, smooth_param,
                                          quantile_keep_pca=25, ensembling_mode="median"):
     """Single-view EKS for one keypoint (the reference
@@ -110,4 +141,4 @@ def ensemble_kalman_smoother_single_view(markers_list, keypoint_ensemble, smooth
 
 
 __all__ = ["ensemble_kalman_smoother_multi_cam", "ensemble_kalman_smoother_pupil",
-           "ensemble_kalman_smoother_single_view", "TRACKER"]
+           "ensemble_kalman_smoother_single_view", "pupil_smoothing_sweep", "TRACKER"]

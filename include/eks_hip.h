@@ -148,7 +148,9 @@ int64_t eks_param_len(int n, int r);
  *
  *   obs      member observations, strides as eks_ensemble
  *   params   (B, P) f64 packed models (see eks_param_len)
- *   out      smoothed observations out(b,t,j) = out[b*ob + t*ot + j*oj] (f64)
+ *   out      smoothed observations out(b,t,j) = out[b*ob + t*ot + j*oj] (f64);
+ *            NULL = filter only: just the NLL (requires nll, ms must be NULL),
+ *            e.g. to score candidate models in a parameter sweep
  *   ms       (B, T, r) contiguous smoothed latents, or NULL
  *   nll      (B) or NULL
  *   model_flags  EKS_MODEL_A_IDENTITY / EKS_MODEL_C_IDENTITY: the caller

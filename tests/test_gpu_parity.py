@@ -400,3 +400,40 @@ def test_singleview_entry_point(torch):
     out = res["markers_df"].to_numpy()[:, :2]
     assert np.abs(out - g["out"]).max() < OUT_TOL
     assert np.isfinite(res["nll"])
+
+
+@pytest.mark.parametrize("algo", [1, 2])
+def test_filter_only_nll_matches_oracle(torch, algo):
+    """Filter-only calls (out = NULL): candidate models of one trajectory
+    sharing the member memory (batch stride 0) scored by their NLL."""
+    from eks_amd import batch, synthetic
+    from oracle import eks_oracle as O
+    rng = np.random.default_rng(21)
+    st = synthetic.pupil_obs(rng, 5, 3000).astype(np.float64)  # (E, T, 8)
+    preds, ev = O.ensemble_array(st)
+    grid = [(d, c) for d in (0.9, 0.99, 0.999) for c in (0.95, 0.999)]
+    models = [O.pupil_params(preds, np.diag([d, c, c])) for d, c in grid]
+    stackp = lambda k: np.stack([m[k] for m in models])  # noqa: E731
+    params = batch.pack_params(stackp("m0"), stackp("S0"), stackp("A"), stackp("Q"), stackp("C"),
+                               stackp("means"))
+    obs = torch.from_numpy(st).cuda().permute(1, 0, 2).unsqueeze(0)
+    scores = batch.nll(obs.expand(len(grid), -1, -1, -1), params, n=8, r=3, algo=algo)
+    scores = scores.cpu().numpy()
+    for i, m in enumerate(models):
+        ref = O.compute_nll(preds - m["means"], m["m0"], m["S0"], m["C"], m["A"], m["Q"], ev)
+        assert abs(scores[i] - ref) <= 1e-9 * abs(ref), (grid[i], scores[i], ref)
+
+
+def test_pupil_smoothing_sweep(torch):
+    from eks_amd.fit import PUPIL_KEYS
+    from eks_amd.pupil_smoother import pupil_smoothing_sweep
+    from eks_amd import synthetic
+    st = synthetic.pupil_obs(np.random.default_rng(3), 5, 2000, a=0.99).astype(np.float64)
+    dfs = [pd.DataFrame(st[e], columns=list(PUPIL_KEYS)) for e in range(5)]
+    kps = ["pupil_top_r", "pupil_right_r", "pupil_bottom_r", "pupil_left_r"]
+    res = pupil_smoothing_sweep(dfs, kps, "ensemble-kalman_tracker", [0.9, 0.99, 0.999],
+                                [0.9, 0.99, 0.999])
+    assert res["nll"].shape == (3, 3) and np.isfinite(res["nll"]).all()
+    i, j = np.unravel_index(np.argmin(res["nll"]), res["nll"].shape)
+    assert res["best"] == ([0.9, 0.99, 0.999][i], [0.9, 0.99, 0.999][j])
+    assert res["markers_df"].shape == (2000, 12)
