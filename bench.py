@@ -351,9 +351,8 @@ def main():
     _lib.profile_begin(4 * a.steps)
     for _ in range(a.steps):
         step()
-    kernels = _lib.profile_end()
-    calls_per_step = 2 if a.config == 5 else 1
-    kern_ms = sum(ms for _, ms in kernels) * calls_per_step
+    kernels = [(n, ms / a.steps) for n, ms in _lib.profile_end()]  # per step
+    kern_ms = sum(ms for _, ms in kernels)
     kern_ms_max = dist.max_over_ranks(kern_ms, device=dev)
     units_local = w["units"]
     units_total = dist.sum_over_ranks(units_local, device=dev)

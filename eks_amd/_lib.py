@@ -53,7 +53,7 @@ def profile_begin(max_calls: int) -> None:
 
 
 def profile_end(max_kernels: int = 8):
-    """[(kernel name, average ms per call)] for the profiled eks_smooth calls."""
+    """[(kernel name, total ms)] over the profiled eks_smooth calls."""
     ms = (C.c_double * max_kernels)()
     names = C.create_string_buffer(64 * max_kernels)
     k = load().eks_profile_end(ms, names, max_kernels, 64)

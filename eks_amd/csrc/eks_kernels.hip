@@ -56,7 +56,7 @@ struct Prof {
   static constexpr int kMarks = 8;
   std::vector<hipEvent_t> ev;
   std::vector<int> nmarks;
-  std::vector<std::string> names;
+  std::vector<std::string> names;  // [call * kMarks + mark]: kernel launched after the mark
 };
 static thread_local Prof g_prof;
 
@@ -71,10 +71,7 @@ void prof_mark(hipStream_t s, const char *next_kernel) {
   if (!g_prof.on || g_prof.call < 0 || g_prof.call >= g_prof.max_calls) return;
   if (g_prof.mark >= Prof::kMarks) return;
   hipEventRecord(g_prof.ev[g_prof.call * Prof::kMarks + g_prof.mark], s);
-  if (g_prof.call == 0) {
-    if ((int)g_prof.names.size() <= g_prof.mark) g_prof.names.resize(g_prof.mark + 1);
-    g_prof.names[g_prof.mark] = next_kernel ? next_kernel : "";
-  }
+  g_prof.names[g_prof.call * Prof::kMarks + g_prof.mark] = next_kernel ? next_kernel : "";
   ++g_prof.mark;
   g_prof.nmarks[g_prof.call] = g_prof.mark;
 }
@@ -388,6 +385,7 @@ int eks_profile_begin(int max_calls) {
   for (auto &e : g_prof.ev)
     if (hipEventCreate(&e) != hipSuccess) return set_err(EKS_ERR_HIP, "hipEventCreate failed");
   g_prof.nmarks.assign(max_calls, 0);
+  g_prof.names.assign((size_t)max_calls * Prof::kMarks, std::string());
   g_prof.max_calls = max_calls;
   g_prof.on = true;
   return EKS_OK;
@@ -397,31 +395,36 @@ int eks_profile_end(double *kernel_ms, char *names, int max_kernels, int name_le
   g_err.clear();
   if (!g_prof.on) return set_err(EKS_ERR_ARG, "eks_profile_end: profiling not started");
   const int calls = g_prof.call + 1;
-  int nk = 0;
-  for (int k = 0; k < max_kernels; ++k) kernel_ms[k] = 0.0;
+  // total milliseconds per kernel name over all recorded calls, in order of
+  // first appearance
+  std::vector<std::string> order;
+  std::vector<double> total;
   for (int c = 0; c < calls; ++c) {
     const int m = g_prof.nmarks[c];
     if (m < 2) continue;
-    nk = std::max(nk, m - 1);
     hipEvent_t *ev = &g_prof.ev[c * Prof::kMarks];
     if (hipEventSynchronize(ev[m - 1]) != hipSuccess)
       return set_err(EKS_ERR_HIP, "hipEventSynchronize failed");
-    for (int k = 0; k + 1 < m && k < max_kernels; ++k) {
+    for (int k = 0; k + 1 < m; ++k) {
       float ms = 0.f;
       hipEventElapsedTime(&ms, ev[k], ev[k + 1]);
-      kernel_ms[k] += ms;
+      const std::string &nm = g_prof.names[c * Prof::kMarks + k];
+      size_t i = 0;
+      while (i < order.size() && order[i] != nm) ++i;
+      if (i == order.size()) {
+        order.push_back(nm);
+        total.push_back(0.0);
+      }
+      total[i] += ms;
     }
   }
-  if (names && name_len > 0) {
-    for (int k = 0; k < std::min(nk, max_kernels); ++k) {
-      const std::string &nm = k < (int)g_prof.names.size() ? g_prof.names[k] : std::string();
-      std::snprintf(names + (size_t)k * name_len, name_len, "%s", nm.c_str());
-    }
-  }
+  const int nk = std::min((int)order.size(), max_kernels);
+  for (int k = 0; k < max_kernels; ++k) kernel_ms[k] = k < nk ? total[k] : 0.0;
+  if (names && name_len > 0)
+    for (int k = 0; k < nk; ++k)
+      std::snprintf(names + (size_t)k * name_len, name_len, "%s", order[k].c_str());
   for (hipEvent_t e : g_prof.ev) hipEventDestroy(e);
-  const int ncalls = calls;
   g_prof = Prof();
-  for (int k = 0; k < std::min(nk, max_kernels); ++k) kernel_ms[k] /= std::max(ncalls, 1);
   return nk;
 }
 

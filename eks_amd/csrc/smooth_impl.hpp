@@ -35,6 +35,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 
 #include "../../include/eks_hip.h"
@@ -69,7 +70,7 @@ struct SmoothArgs {
 // the last partial round of resident blocks (the tail) is a small fraction of
 // the kernel.  EKS_TARGET_LANES overrides it (tuning experiments).
 constexpr long long kTargetLanesDefault = 256LL * 16 * 64;
-constexpr long long kMinChunk = 64;
+constexpr long long kMinChunk = 16;
 
 // above this many chunks per trajectory the chunk scans run one wave per
 // trajectory (EKS_WAVE_SCAN_CHUNKS overrides it: tuning and tests)
@@ -96,10 +97,15 @@ inline int state_len(int r) { return r + r * (r + 1) / 2; }
 
 inline long long round_up(long long x, long long m) { return (x + m - 1) / m * m; }
 
+// Chunk length L: short enough that B * NC lanes fill the GPU (L_fill), but
+// long enough that the chunk scans (which walk ~2 NC / 64 chunks per lane
+// sequentially) stay shorter than a chunk (L_scan = sqrt(2 T / 64)).
 inline long long chunk_len(long long B, long long T, int r) {
   const long long ls = sub_len(r);
   const long long nc = std::max(1LL, (target_lanes() + B - 1) / B);
-  long long L = std::max(kMinChunk, (T + nc - 1) / nc);
+  const long long l_fill = (T + nc - 1) / nc;
+  const long long l_scan = (long long)std::ceil(std::sqrt(2.0 * (double)T / 64.0));
+  long long L = std::max(kMinChunk, std::max(l_fill, l_scan));
   L = round_up(L, ls);
   if (L >= T) L = round_up(T, ls);
   return L;
@@ -318,16 +324,33 @@ constexpr int kBlock = 256;
 
 inline long long blocks_per_chunk(long long B) { return (B + kBlock - 1) / kBlock; }
 
+// UNI (many trajectories): every block lies in one chunk, so c is uniform.
+// !UNI (few trajectories, B << 256): lanes are (chunk, trajectory) pairs in
+// chunk-major order, so one wave spans several chunks and no lane idles.
+template <bool UNI>
 struct Lane {
   long long c;
   unsigned b;
   EKS_DEV bool init(long long B, long long NC) {
-    const long long bpc = (B + kBlock - 1) / kBlock;
-    c = blockIdx.x / bpc;
-    b = (unsigned)((blockIdx.x - c * bpc) * kBlock + threadIdx.x);
-    return c < NC && (long long)b < B;
+    if constexpr (UNI) {
+      const long long bpc = (B + kBlock - 1) / kBlock;
+      c = blockIdx.x / bpc;
+      b = (unsigned)((blockIdx.x - c * bpc) * kBlock + threadIdx.x);
+      return c < NC && (long long)b < B;
+    } else {
+      const long long lane = blockIdx.x * (long long)kBlock + threadIdx.x;
+      if (lane >= NC * B) return false;
+      c = lane / B;
+      b = (unsigned)(lane - c * B);
+      return true;
+    }
   }
 };
+
+inline bool uniform_lanes(long long B) {
+  const long long cap = blocks_per_chunk(B) * kBlock;
+  return (cap - B) * 8 <= cap;  // at most 1/8 of the lanes idle
+}
 
 // element `plane` of a time-major plane array (B values per plane): uniform
 // 64-bit plane base + 32-bit per-lane byte offset, which hipcc lowers to the
@@ -409,10 +432,10 @@ EKS_DEV void c1_stream(const SmoothArgs &a, const ChunkPlan &p, long long s, lon
   }
 }
 
-template <int R, int N, int E, typename T, typename YT, bool AI, bool CI>
+template <int R, int N, int E, typename T, typename YT, bool AI, bool CI, bool UNI>
 __global__ __launch_bounds__(kBlock) void k_c1_elem(SmoothArgs a, ChunkPlan p) {
   constexpr int D = 2;  // member prefetch distance (steps)
-  Lane ln;
+  Lane<UNI> ln;
   const long long B = a.B, TT = a.T;
   if (!ln.init(B, p.NC)) return;
   const long long c = ln.c;
@@ -686,11 +709,11 @@ EKS_DEV void load_yev(const YT *ybuf, const double *evbuf, long long t, long lon
   }
 }
 
-template <int R, int N, typename YT, bool AI, bool CI, int LS>
+template <int R, int N, typename YT, bool AI, bool CI, int LS, bool UNI>
 __global__ __launch_bounds__(kBlock) void k_c3_rerun(SmoothArgs a, ChunkPlan p) {
   constexpr int D = 4;  // y / ev prefetch distance (steps); divides LS
   static_assert(LS % D == 0, "prefetch distance must divide the checkpoint interval");
-  Lane ln;
+  Lane<UNI> ln;
   const long long B = a.B, TT = a.T;
   if (!ln.init(B, p.NC)) return;
   const long long c = ln.c;
@@ -841,9 +864,9 @@ __global__ __launch_bounds__(64) void k_c4_nll(SmoothArgs a, ChunkPlan p) {
   a.nll[b] = s;
 }
 
-template <int R, int N, typename YT, bool AI, bool CI, int LS>
+template <int R, int N, typename YT, bool AI, bool CI, int LS, bool UNI>
 __global__ __launch_bounds__(kBlock) void k_c5_final(SmoothArgs a, ChunkPlan p) {
-  Lane ln;
+  Lane<UNI> ln;
   const long long B = a.B, TT = a.T;
   if (!ln.init(B, p.NC)) return;
   const long long c = ln.c;
@@ -957,12 +980,26 @@ int launch_shape(const SmoothArgs &a, int algo, long long L) {
   }
   ChunkPlan p = make_plan(a.B, a.T, R, N, L);
   p.smooth = a.out != nullptr;
-  const unsigned g256 = (unsigned)(p.NC * blocks_per_chunk(a.B));
+  const bool uni = uniform_lanes(a.B);
+  const unsigned gch = uni ? (unsigned)(p.NC * blocks_per_chunk(a.B))
+                           : grid_for(p.NC * a.B, kBlock);
   const unsigned g64 = grid_for(a.B, 64);
   // y is stored as float when it is exactly a member value (odd-E median of f32)
   const bool y32 = f32 && a.median && (a.E == 3 || a.E == 5);
-  auto rest = [&](auto ytag) -> int {
+  auto run = [&](auto tag, auto ytag, auto unitag) -> int {
+    using Tp = decltype(tag);
     using YT = decltype(ytag);
+    constexpr bool U = decltype(unitag)::value;
+    constexpr int LS = R <= 2 ? 8 : 4;
+    int rc = dispatch_members_c(a.E, [&](auto Ec) {
+      constexpr int EE = decltype(Ec)::value;
+      prof_call_begin();
+      prof_mark(a.stream, "k_c1_elem");
+      hipLaunchKernelGGL((k_c1_elem<R, N, EE, Tp, YT, AI, CI, U>), dim3(gch), dim3(kBlock), 0,
+                         a.stream, a, p);
+      return check_launch("k_c1_elem");
+    });
+    if (rc) return rc;
     // the chunk scans: one lane per trajectory while the chain is short, one
     // wave per trajectory (log-depth scan) when it is long
     const bool wave_scan = p.NC > wave_scan_chunks();
@@ -971,12 +1008,11 @@ int launch_shape(const SmoothArgs &a, int algo, long long L) {
       hipLaunchKernelGGL((k_c2_fscan_w<R, N>), dim3((unsigned)a.B), dim3(64), 0, a.stream, a, p);
     else
       hipLaunchKernelGGL((k_c2_fscan<R, N>), dim3(g64), dim3(64), 0, a.stream, a, p);
-    if (int rc = check_launch("k_c2_fscan")) return rc;
+    if ((rc = check_launch("k_c2_fscan"))) return rc;
     prof_mark(a.stream, "k_c3_rerun");
-    constexpr int LS3 = R <= 2 ? 8 : 4;
-    hipLaunchKernelGGL((k_c3_rerun<R, N, YT, AI, CI, LS3>), dim3(g256), dim3(kBlock), 0, a.stream,
-                       a, p);
-    if (int rc = check_launch("k_c3_rerun")) return rc;
+    hipLaunchKernelGGL((k_c3_rerun<R, N, YT, AI, CI, LS, U>), dim3(gch), dim3(kBlock), 0,
+                       a.stream, a, p);
+    if ((rc = check_launch("k_c3_rerun"))) return rc;
     if (!p.smooth) {  // filter only: sum the NLL shares, no backward pass
       prof_mark(a.stream, "k_c4_nll");
       hipLaunchKernelGGL((k_c4_nll<R>), dim3(g64), dim3(64), 0, a.stream, a, p);
@@ -988,33 +1024,18 @@ int launch_shape(const SmoothArgs &a, int algo, long long L) {
       hipLaunchKernelGGL((k_c4_bscan_w<R>), dim3((unsigned)a.B), dim3(64), 0, a.stream, a, p);
     else
       hipLaunchKernelGGL((k_c4_bscan<R>), dim3(g64), dim3(64), 0, a.stream, a, p);
-    if (int rc = check_launch("k_c4_bscan")) return rc;
-    constexpr int LS = R <= 2 ? 8 : 4;
+    if ((rc = check_launch("k_c4_bscan"))) return rc;
     prof_mark(a.stream, "k_c5_final");
-    hipLaunchKernelGGL((k_c5_final<R, N, YT, AI, CI, LS>), dim3(g256), dim3(kBlock), 0, a.stream,
-                       a, p);
+    hipLaunchKernelGGL((k_c5_final<R, N, YT, AI, CI, LS, U>), dim3(gch), dim3(kBlock), 0,
+                       a.stream, a, p);
     prof_call_end(a.stream);
     return check_launch("k_c5_final");
   };
-  auto k1 = [&](auto tag, auto ytag) -> int {
-    using Tp = decltype(tag);
-    using YT = decltype(ytag);
-    return dispatch_members_c(a.E, [&](auto Ec) {
-      constexpr int EE = decltype(Ec)::value;
-      prof_call_begin();
-      prof_mark(a.stream, "k_c1_elem");
-      hipLaunchKernelGGL((k_c1_elem<R, N, EE, Tp, YT, AI, CI>), dim3(g256), dim3(kBlock), 0,
-                         a.stream, a, p);
-      return check_launch("k_c1_elem");
-    });
+  auto with_uni = [&](auto tag, auto ytag) -> int {
+    return uni ? run(tag, ytag, std::true_type{}) : run(tag, ytag, std::false_type{});
   };
-  int rc;
-  if (y32) {
-    rc = k1(float{}, float{});
-    return rc ? rc : rest(float{});
-  }
-  rc = f32 ? k1(float{}, double{}) : k1(double{}, double{});
-  return rc ? rc : rest(double{});
+  if (y32) return with_uni(float{}, float{});
+  return f32 ? with_uni(float{}, double{}) : with_uni(double{}, double{});
 }
 
 // per-shape entry points (defined in eks_shape_*.hip)

@@ -27,7 +27,7 @@ def test_limits_and_sizes():
     assert lib.eks_smooth_workspace_bytes(10, 100, 2, 2, 5, 1) >= 10 * 100 * 5 * 8
     # time-parallel plan: few long trajectories are cut into chunks
     L = lib.eks_smooth_chunk_len(17, 100000, 2)
-    assert 64 <= L < 100000 and L % 8 == 0
+    assert 16 <= L < 100000 and L % 8 == 0
     assert lib.eks_smooth_chunk_len(1 << 20, 1000, 2) == 0  # enough trajectories: sequential
     assert lib.eks_smooth_workspace_bytes(17, 100000, 2, 2, 5, 2) >= 17 * 100000 * 2 * 16
 
