@@ -91,7 +91,10 @@ inline long long target_lanes() {
   return v;
 }
 
-inline int sub_len(int r) { return r <= 2 ? 8 : 4; }
+// checkpoint interval LS of K3/K5 (steps): K5 keeps LS steps of (J_t, d_t)
+// in registers, so it shrinks as the state / observation grow.
+constexpr int sub_len_c(int r, int n) { return (r <= 2 && n <= 2) ? 8 : (n <= 4 ? 4 : 2); }
+inline int sub_len(int r, int n) { return sub_len_c(r, n); }
 inline int elem_len(int r) { return r * r + r + r * (r + 1) / 2 + r + r * (r + 1) / 2; }
 inline int state_len(int r) { return r + r * (r + 1) / 2; }
 
@@ -101,7 +104,8 @@ inline long long round_up(long long x, long long m) { return (x + m - 1) / m * m
 // long enough that the chunk scans (which walk ~2 NC / 64 chunks per lane
 // sequentially) stay shorter than a chunk (L_scan = sqrt(2 T / 64)).
 inline long long chunk_len(long long B, long long T, int r) {
-  const long long ls = sub_len(r);
+  (void)r;
+  const long long ls = 8;  // a multiple of every checkpoint interval
   const long long nc = std::max(1LL, (target_lanes() + B - 1) / B);
   const long long l_fill = (T + nc - 1) / nc;
   const long long l_scan = (long long)std::ceil(std::sqrt(2.0 * (double)T / 64.0));
@@ -115,6 +119,10 @@ struct ChunkPlan {
   long long L = 0, NC = 0, NSUB = 0;
   int LS = 8;
   int smooth = 1;  // 0: filter only (out == NULL): NLL, no backward pass
+  // members shared by all trajectories (batch stride 0, e.g. candidate models
+  // of one trajectory): y / ev are stored once, as a single plane column
+  long long yB = 0;
+  EKS_DEV unsigned ylane(unsigned b) const { return yB == 1 ? 0u : b; }
   size_t y_off = 0, ev_off = 0, elem_off = 0, cstart_off = 0, bwd_off = 0, nllp_off = 0,
          msend_off = 0, ckpt_off = 0, total = 0;
 };
@@ -123,7 +131,7 @@ inline size_t align256(size_t x) { return (x + 255) / 256 * 256; }
 
 inline ChunkPlan make_plan(long long B, long long T, int r, int n, long long L) {
   ChunkPlan p;
-  p.LS = sub_len(r);
+  p.LS = sub_len(r, n);
   p.L = L;
   p.NC = (T + L - 1) / L;
   p.NSUB = L / p.LS;
@@ -422,8 +430,10 @@ EKS_DEV void c1_stream(const SmoothArgs &a, const ChunkPlan &p, long long s, lon
         reduce_step<E, N, T>(cur, pt, a.se, a.sj, a.E, median, avg, rv);
 #pragma unroll
         for (int j = 0; j < N; ++j) {
-          pl(ybuf, t * N + j, B, b) = (YT)avg[j];
-          pl(evbuf, t * N + j, B, b) = rv[j];
+          if (p.yB != 1 || b == 0) {
+            pl(ybuf, t * N + j, p.yB, p.ylane(b)) = (YT)avg[j];
+            pl(evbuf, t * N + j, p.yB, p.ylane(b)) = rv[j];
+          }
           y[j] = avg[j] - off[j];
         }
         absorb(t, y, rv);
@@ -434,7 +444,7 @@ EKS_DEV void c1_stream(const SmoothArgs &a, const ChunkPlan &p, long long s, lon
 
 template <int R, int N, int E, typename T, typename YT, bool AI, bool CI, bool UNI>
 __global__ __launch_bounds__(kBlock) void k_c1_elem(SmoothArgs a, ChunkPlan p) {
-  constexpr int D = 2;  // member prefetch distance (steps)
+  constexpr int D = (E > 0 && E * N <= 16) ? 2 : 1;  // member prefetch distance (steps)
   Lane<UNI> ln;
   const long long B = a.B, TT = a.T;
   if (!ln.init(B, p.NC)) return;
@@ -711,7 +721,7 @@ EKS_DEV void load_yev(const YT *ybuf, const double *evbuf, long long t, long lon
 
 template <int R, int N, typename YT, bool AI, bool CI, int LS, bool UNI>
 __global__ __launch_bounds__(kBlock) void k_c3_rerun(SmoothArgs a, ChunkPlan p) {
-  constexpr int D = 4;  // y / ev prefetch distance (steps); divides LS
+  constexpr int D = LS < 4 ? LS : 4;  // y / ev prefetch distance (steps); divides LS
   static_assert(LS % D == 0, "prefetch distance must divide the checkpoint interval");
   Lane<UNI> ln;
   const long long B = a.B, TT = a.T;
@@ -740,7 +750,7 @@ __global__ __launch_bounds__(kBlock) void k_c3_rerun(SmoothArgs a, ChunkPlan p) 
   double er[D][N];
 #pragma unroll
   for (int q = 0; q < D; ++q)
-    if (s + q < e) load_yev<N, YT>(ybuf, evbuf, s + q, B, b, yr[q], er[q]);
+    if (s + q < e) load_yev<N, YT>(ybuf, evbuf, s + q, p.yB, p.ylane(b), yr[q], er[q]);
   long long k = 0;
   for (long long t0 = s; t0 < e; t0 += LS, ++k) {
     if (p.smooth) store_state_pl<R>(ckpt, (c * p.NSUB + k) * KS, B, b, m, P);  // state before t0
@@ -754,7 +764,8 @@ __global__ __launch_bounds__(kBlock) void k_c3_rerun(SmoothArgs a, ChunkPlan p) 
           y[j] = (double)yr[q % D][j] - md.off[j];
           rv[j] = er[q % D][j];
         }
-        if (t + D < e) load_yev<N, YT>(ybuf, evbuf, t + D, B, b, yr[q % D], er[q % D]);
+        if (t + D < e)
+          load_yev<N, YT>(ybuf, evbuf, t + D, p.yB, p.ylane(b), yr[q % D], er[q % D]);
         if (t > 0) kf_predict<R, AI>(m, P, md.A, md.Q);
         kf_update<R, N, CI>(m, P, md.C, y, rv, acc, ok);
         if (!p.smooth) continue;
@@ -853,15 +864,19 @@ __global__ __launch_bounds__(64) void k_c4_bscan(SmoothArgs a, ChunkPlan p) {
 }
 
 // filter-only calls (no `out`): the NLL of each trajectory is the sum of its
-// chunks' shares, in chunk order
+// chunks' shares; one wave per trajectory, lane l sums chunks l, l+64, ...,
+// then a fixed-order shuffle tree (deterministic)
 template <int R>
 __global__ __launch_bounds__(64) void k_c4_nll(SmoothArgs a, ChunkPlan p) {
-  const long long b = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  const long long b = blockIdx.x;
+  const int l = threadIdx.x;
   if (b >= a.B || !a.nll) return;
   const double *np_ = (const double *)(a.ws + p.nllp_off);
   double s = 0.0;
-  for (long long c = 0; c < p.NC; ++c) s += np_[c * a.B + b];
-  a.nll[b] = s;
+  for (long long c = l; c < p.NC; c += 64) s += np_[c * a.B + b];
+#pragma unroll
+  for (int k = 32; k >= 1; k >>= 1) s += __shfl_xor(s, k, 64);
+  if (l == 0) a.nll[b] = s;
 }
 
 template <int R, int N, typename YT, bool AI, bool CI, int LS, bool UNI>
@@ -899,7 +914,7 @@ __global__ __launch_bounds__(kBlock) void k_c5_final(SmoothArgs a, ChunkPlan p) 
     double er[LS][N];
 #pragma unroll
     for (int j = 0; j < LS; ++j)
-      if (t0 + j < e) load_yev<N, YT>(ybuf, evbuf, t0 + j, B, b, yr[j], er[j]);
+      if (t0 + j < e) load_yev<N, YT>(ybuf, evbuf, t0 + j, p.yB, p.ylane(b), yr[j], er[j]);
     double Jr[LS][R][R], dr[LS][R];
 #pragma unroll
     for (int j = 0; j < LS; ++j) {
@@ -980,6 +995,7 @@ int launch_shape(const SmoothArgs &a, int algo, long long L) {
   }
   ChunkPlan p = make_plan(a.B, a.T, R, N, L);
   p.smooth = a.out != nullptr;
+  p.yB = (a.sb == 0 && a.B > 1) ? 1 : a.B;
   const bool uni = uniform_lanes(a.B);
   const unsigned gch = uni ? (unsigned)(p.NC * blocks_per_chunk(a.B))
                            : grid_for(p.NC * a.B, kBlock);
@@ -990,7 +1006,7 @@ int launch_shape(const SmoothArgs &a, int algo, long long L) {
     using Tp = decltype(tag);
     using YT = decltype(ytag);
     constexpr bool U = decltype(unitag)::value;
-    constexpr int LS = R <= 2 ? 8 : 4;
+    constexpr int LS = sub_len_c(R, N);
     int rc = dispatch_members_c(a.E, [&](auto Ec) {
       constexpr int EE = decltype(Ec)::value;
       prof_call_begin();
@@ -1015,7 +1031,7 @@ int launch_shape(const SmoothArgs &a, int algo, long long L) {
     if ((rc = check_launch("k_c3_rerun"))) return rc;
     if (!p.smooth) {  // filter only: sum the NLL shares, no backward pass
       prof_mark(a.stream, "k_c4_nll");
-      hipLaunchKernelGGL((k_c4_nll<R>), dim3(g64), dim3(64), 0, a.stream, a, p);
+      hipLaunchKernelGGL((k_c4_nll<R>), dim3((unsigned)a.B), dim3(64), 0, a.stream, a, p);
       prof_call_end(a.stream);
       return check_launch("k_c4_nll");
     }
