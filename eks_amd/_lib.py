@@ -43,6 +43,8 @@ SIGNATURES = {
     "eks_smooth": (_i32, [_p, _i32, _i64, _i64, _i32, _i32, _i32, _i64, _i64, _i64, _i64, _i32,
                           _p, _p, _i64, _i64, _i64, _p, _p, _p, _sz, _i32, _i32, _p, _p]),
     "eks_smooth_chunk_len": (_i64, [_i64, _i64, _i32]),
+    "eks_newton_filter": (_i32, [_i64, _i64, _i32, _i32, _p, _p, _p, _p, _p, _p, _p, _i32, _i32,
+                                 _p, _p, _p]),
     "eks_profile_begin": (_i32, [_i32]),
     "eks_profile_end": (_i32, [_p, _p, _i32, _i32]),
 }

@@ -17,6 +17,7 @@ constexpr int kMaxMembers = 64; // E
 
 int set_err(int code, const char *fmt, ...);
 int check_launch(const char *what);
+void clear_err();
 
 // Optional per-kernel timing (eks_profile_begin/end): records a hipEvent on
 // the launch stream before each kernel of an eks_smooth call and after the

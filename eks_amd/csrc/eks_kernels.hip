@@ -47,6 +47,8 @@ int set_err(int code, const char *fmt, ...) {
   return code;
 }
 
+void clear_err() { g_err.clear(); }
+
 // ------------------------------------------------------------------------
 // per-kernel timing of eks_smooth calls (profiling aid)
 // ------------------------------------------------------------------------

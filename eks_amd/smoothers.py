@@ -3,6 +3,8 @@
     ensemble_kalman_smoother_multi_cam   eks/multiview_pca_smoother.py:611-767
     ensemble_kalman_smoother_pupil       eks/pupil_smoother.py:82-223
     ensemble_kalman_smoother_single_view build definition
+    eks_opti_smoother_multi_cam          eks/multiview_pca_smoother.py:777-933
+    eks_opti_smoother_pupil              eks/pupil_smoother.py:227-320
 
 Flow for one keypoint: member DataFrames -> (E, T, n) array -> GPU ensemble
 (eks_ensemble) -> host model fit (eks_amd.fit) -> GPU fused smoother
@@ -15,6 +17,7 @@ import numpy as np
 import pandas as pd
 
 from . import _lib, batch, core, fit
+from .newton_eks import kalman_newton_recursive
 from .utils import TRACKER, make_dlc_pandas_index
 
 
@@ -142,3 +145,63 @@ def ensemble_kalman_smoother_single_view(markers_list, keypoint_ensemble, smooth
 
 __all__ = ["ensemble_kalman_smoother_multi_cam", "ensemble_kalman_smoother_pupil",
            "ensemble_kalman_smoother_single_view", "pupil_smoothing_sweep", "TRACKER"]
+
+
+def _camera_dfs(out, keypoint_ensemble, camera_names):
+    pdindex = make_dlc_pandas_index([keypoint_ensemble])
+    nan = np.full(out.shape[0], np.nan)
+    return {cam + "_df": pd.DataFrame(np.stack([out[:, 2 * c], out[:, 2 * c + 1], nan], axis=1),
+                                      columns=pdindex)
+            for c, cam in enumerate(camera_names)}
+
+
+def eks_opti_smoother_multi_cam(markers_list_cameras, keypoint_ensemble, smooth_param,
+                                quantile_keep_pca, camera_names, plot=False):
+    """Multi-view PCA model + Newton forward filter, no backward pass
+    (eks/multiview_pca_smoother.py:777-933): the model fit of
+    ensemble_kalman_smoother_multi_cam, then kalman_newton_recursive with
+    B = PCA axes, E = smooth_param * cov(diff(pcs)), output B q + means.
+    ``plot`` is accepted for signature compatibility; the reference's plot
+    branch reads a developer-local file, so nothing is plotted."""
+    V = len(camera_names)
+    if V < 2:
+        raise ValueError("eks_opti_smoother_multi_cam needs at least two cameras")
+    n_models = len(markers_list_cameras[0])
+    cols = [np.stack([np.asarray(markers_list_cameras[c][e].to_numpy()[:, :2], dtype=np.float64)
+                      for e in range(n_models)]) for c in range(V)]
+    stack = np.concatenate(cols, axis=2)
+    preds, ev = core.ensemble_array(stack)
+    model = fit.multicam_model(preds, ev, smooth_param, quantile_keep_pca)
+    q = kalman_newton_recursive(preds - model["offset"], model["m0"], model["S0"], model["A"],
+                                model["C"], ev, model["Q"])
+    out = q @ model["C"].T + model["offset"]
+    return _camera_dfs(out, keypoint_ensemble, camera_names)
+
+
+def eks_opti_smoother_pupil(markers_list, keypoint_names, tracker_name, state_transition_matrix,
+                            plot=False):
+    """IBL pupil model + Newton forward filter (eks/pupil_smoother.py:227-320).
+
+    As in the reference, the transition matrix is fixed at A = 0.99 I (:260)
+    and ``state_transition_matrix`` is ignored.  The reference's plot=False
+    branch then uses an undefined variable; this returns what its plot=True
+    branch and the committed data/misc/pupil-test/opti_eks_latents.csv hold:
+    markers_df (C q + offsets, order top, right, bottom, left, NaN likelihood)
+    and latents_df (diameter, com_x, com_y)."""
+    stack = np.stack([np.stack([np.asarray(df[k], dtype=np.float64) for k in fit.PUPIL_KEYS], 1)
+                      for df in markers_list])
+    preds, ev = core.ensemble_array(stack)
+    model = fit.pupil_model(preds, np.diag([0.99, 0.99, 0.99]))
+    q = kalman_newton_recursive(preds - model["offset"], model["m0"], model["S0"], model["A"],
+                                model["C"], ev, model["Q"])
+    out = q @ model["C"].T + model["offset"]
+    by_key = {k: out[:, j] for j, k in enumerate(fit.PUPIL_KEYS)}
+    nan = np.full(out.shape[0], np.nan)
+    cols = []
+    for kp in ('top', 'right', 'bottom', 'left'):
+        cols += [by_key[f'pupil_{kp}_r_x'], by_key[f'pupil_{kp}_r_y'], nan]
+    markers_df = pd.DataFrame(np.stack(cols, 1), columns=make_dlc_pandas_index(keypoint_names))
+    lat = np.stack([q[:, 0], q[:, 1] + model["mx"], q[:, 2] + model["my"]], 1)
+    idx = pd.MultiIndex.from_arrays([[tracker_name] * 3, ['diameter', 'com_x', 'com_y']],
+                                    names=('scorer', 'latent'))
+    return {'markers_df': markers_df, 'latents_df': pd.DataFrame(lat, columns=idx)}

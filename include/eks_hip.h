@@ -175,6 +175,26 @@ int eks_smooth(const void *obs, int obs_dtype, int64_t B, int64_t T, int E, int 
 int64_t eks_smooth_chunk_len(int64_t B, int64_t T, int r);
 
 /*
+ * eks_newton_filter -- replaces eks/newton_eks.py:115-148
+ * `kalman_newton_recursive(y, mu0, S0, A, B, ensemble_vars, E, max_iter)`
+ * for B trajectories (one lane each): information-form filter with
+ * q[0] = mu0, P0 = inv(S0), D_t = diag(ensemble_vars[t]), P carried over
+ * between the max_iter iterations, q updated in place.
+ *   y, ev   (B, T, n) f64 contiguous (centred observations, ensemble variances)
+ *   mu0 (r), S0 (r, r), A (r, r), Bm (n, r), E (r, r): per trajectory
+ *           (b-strided) or, with params_shared = 1, one model for all
+ *   q       (B, T, r) f64 output
+ *   status  (B) int32 or NULL: EKS_STATUS_SINGULAR where the reference's
+ *           np.linalg.inv would raise (zero variance, singular S0 / info).
+ * The reference's loss vector is identically 0 (q is updated in place), so
+ * it is not produced here.
+ */
+int eks_newton_filter(int64_t B, int64_t T, int n, int r, const double *y, const double *ev,
+                      const double *mu0, const double *S0, const double *A, const double *Bm,
+                      const double *E, int params_shared, int max_iter, double *q,
+                      int32_t *status, void *stream);
+
+/*
  * Profiling aid (not part of the smoother's semantics).  After
  * eks_profile_begin(max_calls), each eks_smooth call on this thread records
  * a hipEvent on its stream before each of its kernels and after the last one

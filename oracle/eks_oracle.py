@@ -337,3 +337,61 @@ def pupil_smooth(stack, A, mode="median"):
     markers = ms @ p["C"].T + p["means"]
     latents = np.stack([ms[:, 0], ms[:, 1] + p["mx"], ms[:, 2] + p["my"]], axis=1)
     return markers, latents, p, ev
+
+
+# --------------------------------------------------------------------------
+# F3  Newton "opti" forward filter  (eks/newton_eks.py:115-148)
+# --------------------------------------------------------------------------
+def kalman_newton_recursive(y, mu0, S0, A, B, ensemble_vars, E, max_iter=1):
+    """Information-form forward filter of eks/newton_eks.py:115-148 with its
+    quirks: q[0] = mu0 with no measurement update, P starts as inv(S0) (used
+    as a covariance), P carries over between iterations, and q is updated in
+    place (the reference's ``qnew = q`` alias), so every iteration's loss is 0.
+    For T == 1 the trailing step reads q[T-2] = q[-1] = q[0]."""
+    T = y.shape[0]
+    q = np.zeros((T, mu0.shape[0]))
+    q[0] = mu0
+    P = np.linalg.inv(S0)
+    loss = np.zeros(max_iter)
+    for it in range(max_iter):
+        for t in range(1, T):
+            invD = np.linalg.inv(np.diag(ensemble_vars[t]))
+            P = np.linalg.inv(np.linalg.inv(E + A @ P @ A.T) + B.T @ invD @ B)
+            q[t] = A @ q[t - 1] - P @ B.T @ invD @ (B @ A @ q[t - 1] - y[t])
+        if T == 1:  # the reference's separate last step with q[T-2] == q[-1]
+            invD = np.linalg.inv(np.diag(ensemble_vars[0]))
+            P = np.linalg.inv(np.linalg.inv(E + A @ P @ A.T) + B.T @ invD @ B)
+            q[0] = A @ q[0] - P @ B.T @ invD @ (B @ A @ q[0] - y[0])
+        loss[it] = 0.0
+    if max_iter == 1:
+        return q
+    return q, loss
+
+
+def multicam_opti_smooth(cam_stacks, smooth_param, quantile_keep, mode="median"):
+    """eks_opti_smoother_multi_cam (eks/multiview_pca_smoother.py:777-933):
+    the multicam model fit, then the Newton filter (no backward pass)."""
+    preds, ev = [], []
+    for st in cam_stacks:
+        p_, v_ = ensemble_array(st, mode)
+        preds.append(p_)
+        ev.append(v_)
+    preds = np.hstack(preds)
+    ev = np.hstack(ev)
+    p = multicam_params(preds, ev, smooth_param, quantile_keep)
+    q = kalman_newton_recursive(p["y"], p["m0"], p["S0"], p["A"], p["C"], ev, p["Q"])
+    return q @ p["C"].T + p["means"], p, q
+
+
+def pupil_opti_smooth(stack, mode="median"):
+    """eks_opti_smoother_pupil (eks/pupil_smoother.py:227-320) as intended:
+    the pupil model with the hard-coded A = 0.99 I (:260), Newton filter,
+    latents = (diameter, com_x + mx, com_y + my) and markers = C q + offsets.
+    (The reference's plot=False branch references an undefined q; the committed
+    data/misc/pupil-test/opti_eks_latents.csv is this computation.)"""
+    preds, ev = ensemble_array(stack, mode)
+    p = pupil_params(preds, np.diag([0.99, 0.99, 0.99]))
+    q = kalman_newton_recursive(p["y"], p["m0"], p["S0"], p["A"], p["C"], ev, p["Q"])
+    markers = q @ p["C"].T + p["means"]
+    latents = np.stack([q[:, 0], q[:, 1] + p["mx"], q[:, 2] + p["my"]], axis=1)
+    return markers, latents, p, ev

@@ -107,3 +107,30 @@ def test_nll_matches_dense_definition():
         sig = np.diag(g["ev"][t]) + g["C"] @ pP @ g["C"].T
         tot -= multivariate_normal(g["C"] @ pm, sig).logpdf(g["y"][t])
     assert abs(nll - tot) < 1e-8 * abs(tot)
+
+
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "newton_*.npz"))),
+                         ids=lambda p: os.path.basename(p)[:-4])
+def test_newton(path):
+    g = np.load(path)
+    it = int(g["max_iter"])
+    res = O.kalman_newton_recursive(g["y"], g["mu0"], g["S0"], g["A"], g["B"], g["ev"], g["E"],
+                                    max_iter=it)
+    q = res if it == 1 else res[0]
+    if it > 1:
+        assert np.all(res[1] == 0.0)  # the reference's in-place alias makes the loss 0
+    np.testing.assert_allclose(q, g["q"], rtol=0, atol=1e-9 * max(1.0, np.abs(g["q"]).max()))
+
+
+def test_newton_multicam_opti():
+    g = np.load(os.path.join(GOLDEN, "opti_mouse_paw2LF.npz"))
+    out, _, _ = O.multicam_opti_smooth(list(g["stacks"]), float(g["s"]), float(g["q"]))
+    np.testing.assert_allclose(out, g["out"], rtol=0, atol=1e-8)
+    np.testing.assert_allclose(out, g["golden"], rtol=0, atol=1e-8)
+
+
+def test_newton_pupil_opti():
+    g = np.load(os.path.join(GOLDEN, "opti_pupil_ibl.npz"))
+    _, latents, _, _ = O.pupil_opti_smooth(g["stack"])
+    np.testing.assert_allclose(latents, g["latents"], rtol=0, atol=1e-9)
+    np.testing.assert_allclose(latents, g["golden_latents"], rtol=0, atol=1e-9)

@@ -242,14 +242,92 @@ def gen_pupil(ps, ut):
           golden_latents=g_lat, keypoint_names=np.array(kps))
 
 
+def gen_newton(mv, ps, ut):
+    """kalman_newton_recursive (eks/newton_eks.py:115) on random systems, the
+    mirror-mouse opti golden (eks_opti.csv) and the pupil opti golden."""
+    import eks.newton_eks as ne
+    for i, (r, n, T, it) in enumerate([(2, 2, 1, 1), (2, 2, 2, 1), (3, 4, 200, 1), (3, 8, 300, 1),
+                                       (2, 2, 300, 3), (3, 6, 100, 2)]):
+        rng = np.random.default_rng(3000 + i)
+        A = np.eye(r) + 0.05 * rng.normal(size=(r, r))
+        E = _spd(rng, r, 0.5)
+        S0 = _spd(rng, r, 20.0)
+        mu0 = rng.normal(size=r)
+        B = rng.normal(size=(n, r)) * 2.0
+        x = np.cumsum(rng.normal(size=(T, r)), axis=0)
+        y = x @ B.T + rng.normal(size=(T, n))
+        ev = rng.uniform(0.05, 4.0, size=(T, n))
+        res = ne.kalman_newton_recursive(y, mu0, S0, A, B, ev, E, max_iter=it)
+        q = res if it == 1 else res[0]
+        _save(f"newton_r{r}_n{n}_T{T}_it{it}", y=y, mu0=mu0, S0=S0, A=A, B=B, ev=ev, E=E,
+              max_iter=it, q=q)
+    # mirror-mouse opti golden: eks_opti_smoother_multi_cam(..., 0.01, 25, plot=False)
+    markers = _mouse_markers(ut)
+    cams = ["top", "bot"]
+    golden = pd.read_csv(os.path.join(REF, "data/mirror-mouse/output/eks_opti.csv"),
+                         header=[0, 1, 2], index_col=0)
+    for paw in ("paw2LF",):
+        by_cam, stacks = [[] for _ in cams], []
+        for c, cam in enumerate(cams):
+            cols = [f"{paw}_{cam}_x", f"{paw}_{cam}_y"]
+            for m in markers:
+                by_cam[c].append(m[cols])
+            stacks.append(np.stack([m[cols].to_numpy() for m in markers]))
+        dfs = mv.eks_opti_smoother_multi_cam(by_cam, paw, 0.01, 25, cams, plot=False)
+        out = np.concatenate(
+            [dfs[f"{cam}_df"].loc[:, ("ensemble-kalman_tracker", paw, c)].to_numpy()[:, None]
+             for cam in cams for c in ("x", "y")], axis=1)
+        gold = np.concatenate(
+            [golden.loc[:, ("ensemble-kalman_tracker", f"{paw}_{cam}", c)].to_numpy()[:, None]
+             for cam in cams for c in ("x", "y")], axis=1)
+        print(f"  opti {paw}: re-run vs committed golden max|d| = {np.abs(out - gold).max():.2e}")
+        _save(f"opti_mouse_{paw}", stacks=np.stack(stacks), s=0.01, q=25.0, out=out, golden=gold)
+    # pupil opti golden: the Newton filter with the pupil model and A = 0.99 I
+    # (eks/pupil_smoother.py:227-320), committed as data/misc/pupil-test/opti_eks_latents.csv
+    files = sorted(glob.glob(os.path.join(REF, "data/ibl-pupil/*.csv")))
+    mk = []
+    for f in files:
+        df = pd.read_csv(f, header=[0, 1, 2], index_col=0)
+        kps = [c[1] for c in df.columns[::3]]
+        mk.append(ut.convert_lp_dlc(df, kps, model_name=df.columns[0][0]))
+    keys = ['pupil_top_r_x', 'pupil_top_r_y', 'pupil_bottom_r_x', 'pupil_bottom_r_y',
+            'pupil_right_r_x', 'pupil_right_r_y', 'pupil_left_r_x', 'pupil_left_r_y']
+    import eks.ensemble_kalman as ek
+    preds, ev, _, avg_d, _, _ = ek.ensemble(mk, keys)
+    loc = ps.get_pupil_location(avg_d)
+    diam = ps.get_pupil_diameter(avg_d)
+    mx, my = loc[:, 0].mean(), loc[:, 1].mean()
+    y = preds.copy()
+    y[:, 0::2] -= mx
+    y[:, 1::2] -= my
+    A = np.diag([0.99, 0.99, 0.99])
+    mu0 = np.array([diam.mean(), 0.0, 0.0])
+    vx, vy = np.var(loc[:, 0] - mx), np.var(loc[:, 1] - my)
+    S0 = np.diag([np.var(diam), vx, vy])
+    E = np.diag([np.var(diam) * (1 - 0.99 ** 2), vx * (1 - 0.99 ** 2), vy * (1 - 0.99 ** 2)])
+    B = np.array([[0, 1, 0], [-.5, 0, 1], [0, 1, 0], [.5, 0, 1], [.5, 1, 0], [0, 0, 1],
+                  [-.5, 1, 0], [0, 0, 1]], dtype=np.float64)
+    q = ne.kalman_newton_recursive(y, mu0, S0, A, B, ev, E)
+    lat = np.stack([q[:, 0], q[:, 1] + mx, q[:, 2] + my], 1)
+    g = pd.read_csv(os.path.join(REF, "data/misc/pupil-test/opti_eks_latents.csv"),
+                    header=[0, 1], index_col=0).to_numpy()
+    print(f"  opti pupil latents vs committed golden max|d| = {np.abs(lat - g).max():.2e}")
+    _save("opti_pupil_ibl", stack=np.stack([m[keys].to_numpy() for m in mk]), A=A, latents=lat,
+          golden_latents=g)
+
+
 def main():
     ek, mv, ps, ut = _import_reference()
+    if len(sys.argv) > 1 and sys.argv[1] == "newton":
+        gen_newton(mv, ps, ut)
+        return
     gen_core(ek)
     gen_ensemble(ek)
     gen_singleview(ek)
     gen_multicam(mv, ut)
     gen_fish(ut, mv)
     gen_pupil(ps, ut)
+    gen_newton(mv, ps, ut)
 
 
 if __name__ == "__main__":
