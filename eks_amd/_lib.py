@@ -13,6 +13,7 @@ import re
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libeks_hip.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "eks_hip.h")
+HEADERS = [HEADER, os.path.join(os.path.dirname(HERE), "include", "eks_io.h")]
 
 EKS_OK, EKS_ERR_ARG, EKS_ERR_UNSUPPORTED, EKS_ERR_HIP = 0, 1, 2, 4
 EKS_STATUS_SINGULAR, EKS_STATUS_BAD_MODEL, EKS_STATUS_SCAN = 1, 2, 4
@@ -46,6 +47,10 @@ SIGNATURES = {
     "eks_newton_filter": (_i32, [_i64, _i64, _i32, _i32, _p, _p, _p, _p, _p, _p, _p, _i32, _i32,
                                  _p, _p, _p]),
     "eks_profile_begin": (_i32, [_i32]),
+    # include/eks_io.h (host-only)
+    "eks_io_last_error": (C.c_char_p, []),
+    "eks_csv_probe": (_i32, [C.c_char_p, _i32, _p, _p, _p]),
+    "eks_csv_read": (_i32, [C.c_char_p, _i32, _p, _i64, _i64, _p, _p, _i64, _i32]),
     "eks_profile_end": (_i32, [_p, _p, _i32, _i32]),
 }
 
@@ -72,8 +77,8 @@ class EksError(RuntimeError):
 
 
 def header_symbols() -> list[str]:
-    """Function names declared in include/eks_hip.h."""
-    src = open(HEADER).read()
+    """Function names declared in include/eks_hip.h and include/eks_io.h."""
+    src = "\n".join(open(h).read() for h in HEADERS)
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(eks_[a-z_0-9]+)\s*\(", src)))
 

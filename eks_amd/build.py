@@ -4,7 +4,8 @@
     python -m eks_amd.build --force  # rebuild everything
 
 Each ``csrc/*.hip`` translation unit is compiled by ``hipcc
---offload-arch=gfx950`` (cross-compiles without a GPU) into an object file,
+--offload-arch=gfx950`` (cross-compiles without a GPU), each host-only
+``csrc/*.cpp`` unit by g++, into an object file,
 then all objects are linked into one shared library with a plain C ABI
 (include/eks_hip.h).  The library is what the Python package binds with
 ctypes; it is built in the tree so that it travels with the repository
@@ -48,8 +49,15 @@ def _stale(target: str, sources: list[str]) -> bool:
     return any(os.path.getmtime(s) > t for s in sources)
 
 
+CXX = shutil.which("g++") or "g++"
+CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", "-pthread", "-Wall"]
+
+
 def _compile(src: str, obj: str) -> None:
-    cmd = [HIPCC, *CFLAGS, "-c", src, "-o", obj]
+    if src.endswith(".cpp"):  # host-only units (CSV I/O)
+        cmd = [CXX, *CXXFLAGS, "-c", src, "-o", obj]
+    else:
+        cmd = [HIPCC, *CFLAGS, "-c", src, "-o", obj]
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
         raise RuntimeError(f"hipcc failed on {src}:\n{res.stderr[-6000:]}")
@@ -57,12 +65,12 @@ def _compile(src: str, obj: str) -> None:
 
 def build(force: bool = False, jobs: int | None = None, verbose: bool = True) -> str:
     os.makedirs(OBJDIR, exist_ok=True)
-    srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+    srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
     deps = _deps()
     todo = []
     objs = []
     for s in srcs:
-        o = os.path.join(OBJDIR, os.path.basename(s)[:-4] + ".o")
+        o = os.path.join(OBJDIR, os.path.splitext(os.path.basename(s))[0] + ".o")
         objs.append(o)
         if force or _stale(o, [s, *deps]):
             todo.append((s, o))
@@ -75,7 +83,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = True) ->
                 fut.result()
     lib = lib_path()
     if todo or _stale(lib, objs):
-        cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", lib + ".tmp"]
+        cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-pthread", "-o", lib + ".tmp"]
         res = subprocess.run(cmd, capture_output=True, text=True)
         if res.returncode != 0:
             raise RuntimeError(f"link failed:\n{res.stderr[-4000:]}")

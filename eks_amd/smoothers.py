@@ -17,7 +17,7 @@ import numpy as np
 import pandas as pd
 
 from . import _lib, batch, core, fit
-from .newton_eks import kalman_newton_recursive
+from .newton_eks import kalman_newton_recursive, newton_filter_batch
 from .utils import TRACKER, make_dlc_pandas_index
 
 
@@ -143,8 +143,6 @@ def ensemble_kalman_smoother_single_view(markers_list, keypoint_ensemble, smooth
     return {'markers_df': df, 'nll': nll}
 
 
-__all__ = ["ensemble_kalman_smoother_multi_cam", "ensemble_kalman_smoother_pupil",
-           "ensemble_kalman_smoother_single_view", "pupil_smoothing_sweep", "TRACKER"]
 
 
 def _camera_dfs(out, keypoint_ensemble, camera_names):
@@ -205,3 +203,61 @@ def eks_opti_smoother_pupil(markers_list, keypoint_names, tracker_name, state_tr
     idx = pd.MultiIndex.from_arrays([[tracker_name] * 3, ['diameter', 'com_x', 'com_y']],
                                     names=('scorer', 'latent'))
     return {'markers_df': markers_df, 'latents_df': pd.DataFrame(lat, columns=idx)}
+
+
+def ensemble_stacks(stacks, mode: str = "median"):
+    """(K, E, T, n) member array of K trajectories -> preds, vars (K, T, n)
+    CUDA float64, one eks_ensemble launch."""
+    torch = _lib.require_gpu()
+    if mode not in ("median", "mean"):
+        raise ValueError(f"{mode} averaging not supported")
+    K, E, T, n = stacks.shape
+    d = torch.from_numpy(np.ascontiguousarray(stacks, dtype=np.float64)).to("cuda")
+    preds = torch.empty((K, T, n), dtype=torch.float64, device="cuda")
+    var = torch.empty_like(preds)
+    lib = _lib.load()
+    _lib.check(lib.eks_ensemble(d.data_ptr(), _lib.EKS_F64, K, T, E, n, E * T * n, n, T * n, 1,
+                                _lib.EKS_MEDIAN if mode == "median" else _lib.EKS_MEAN,
+                                preds.data_ptr(), var.data_ptr(), _lib.stream_ptr()),
+               "eks_ensemble")
+    return d, preds, var
+
+
+def multi_cam_batch(stacks, smooth_param, quantile_keep_pca, version: str = "standard"):
+    """All keypoints of a multi-camera dataset in one launch each for the
+    ensemble and the smoother (the reference loops keypoints one call at a
+    time: scripts/multicam_example.py:106-150).
+
+    stacks (K, E, T, 2V) camera-major (x, y) columns per keypoint.  The
+    per-keypoint model fit is ensemble_kalman_smoother_multi_cam's
+    (eks/multiview_pca_smoother.py:684-731); version "standard" runs the
+    fused RTS smoother (eks_smooth), "opti" the Newton filter
+    (eks_newton_filter, :777-933).  Returns out (K, T, 2V) float64 numpy."""
+    torch = _lib.require_gpu()
+    stacks = np.asarray(stacks, dtype=np.float64)
+    K, E, T, n = stacks.shape
+    if n < 4:
+        raise ValueError("multi-camera smoothing needs at least two cameras")
+    d, preds_d, ev_d = ensemble_stacks(stacks)
+    preds, ev = preds_d.cpu().numpy(), ev_d.cpu().numpy()
+    models = [fit.multicam_model(preds[k], ev[k], smooth_param, quantile_keep_pca)
+              for k in range(K)]
+    st = lambda key: np.stack([m[key] for m in models])  # noqa: E731
+    if version == "opti":
+        y = preds_d - torch.from_numpy(st("offset")).to("cuda")[:, None, :]
+        q, status = newton_filter_batch(y, ev_d, st("m0"), st("S0"), st("A"), st("C"), st("Q"))
+        if bool((status != 0).any()):
+            raise np.linalg.LinAlgError("Singular matrix (kalman_newton_recursive)")
+        q = q.cpu().numpy()
+        return np.einsum("ktr,knr->ktn", q, st("C")) + st("offset")[:, None, :]
+    params = batch.pack_params(st("m0"), st("S0"), st("A"), st("Q"), st("C"), st("offset"))
+    obs = d.permute(0, 2, 1, 3)  # (K, T, E, n) view
+    res = batch.smooth(obs, params, n=n, r=3, flags=batch.model_flags(st("A"), st("C")),
+                       check=True)
+    return res["out"].cpu().numpy()
+
+
+__all__ = ["ensemble_kalman_smoother_multi_cam", "ensemble_kalman_smoother_pupil",
+           "ensemble_kalman_smoother_single_view", "pupil_smoothing_sweep",
+           "eks_opti_smoother_multi_cam", "eks_opti_smoother_pupil", "multi_cam_batch",
+           "ensemble_stacks", "TRACKER"]

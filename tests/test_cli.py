@@ -1,0 +1,95 @@
+"""F1: the command-line scripts end to end on the committed fixture CSVs,
+against the outputs the reference's scripts produce on the same files
+(tests/golden/csv/expected, written by tools/gen_golden.py gen_cli)."""
+import os
+
+import numpy as np
+import pandas as pd
+import pytest
+
+from tests.conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+CSV = os.path.join(GOLDEN, "csv")
+EXP = os.path.join(CSV, "expected")
+TOL = 1e-5  # north-star output tolerance (pixels)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _cmp(ours_path, exp_path, header):
+    ours = pd.read_csv(ours_path, header=header, index_col=0)
+    exp = pd.read_csv(exp_path, header=header, index_col=0)
+    assert list(ours.columns) == list(exp.columns)
+    assert list(ours.index) == list(exp.index)
+    a, b = ours.to_numpy(), exp.to_numpy()
+    assert np.array_equal(np.isnan(a), np.isnan(b))
+    assert np.nanmax(np.abs(a - b)) < TOL
+    with open(ours_path) as f1, open(exp_path) as f2:  # identical header lines
+        for _ in range(len(header)):
+            assert f1.readline() == f2.readline()
+
+
+@pytest.mark.parametrize("version,fname", [("standard", "eks.csv"), ("opti", "eks_opti.csv")])
+def test_multicam_script(tmp_path, version, fname):
+    from eks_amd.scripts import multicam_example
+    multicam_example.main(["--csv-dir", os.path.join(CSV, "mirror-mouse"), "--bodypart-list",
+                           "paw1LH", "paw2LF", "paw3RF", "paw4RH", "--camera-names", "top", "bot",
+                           "--save-dir", str(tmp_path), "--eks_version", version])
+    _cmp(tmp_path / fname, os.path.join(EXP, fname), [0, 1, 2])
+    pdf = "example_eks_opti_result.pdf" if version == "opti" else "example_eks_result.pdf"
+    assert (tmp_path / pdf).exists()
+
+
+@pytest.mark.parametrize("version,prefix", [("standard", "kalman_smoothed"),
+                                            ("opti", "opti_eks")])
+def test_pupil_script(tmp_path, version, prefix):
+    from eks_amd.scripts import pupil_example
+    pupil_example.main(["--csv-dir", os.path.join(CSV, "ibl-pupil"), "--save-dir", str(tmp_path),
+                        "--diameter-s", "0.99", "--com-s", "0.99", "--eks_version", version,
+                        "--no-plot"])
+    _cmp(tmp_path / f"{prefix}_pupil_traces.csv",
+         os.path.join(EXP, f"{prefix}_pupil_traces.csv"), [0, 1, 2])
+    _cmp(tmp_path / f"{prefix}_latents.csv", os.path.join(EXP, f"{prefix}_latents.csv"), [0, 1])
+
+
+def test_pupil_script_sweep(tmp_path):
+    from eks_amd.scripts import pupil_example
+    pupil_example.main(["--csv-dir", os.path.join(CSV, "ibl-pupil"), "--save-dir", str(tmp_path),
+                        "--eks_version", "standard", "--sweep", "0.9,0.99", "0.95,0.99",
+                        "--no-plot"])
+    assert (tmp_path / "kalman_smoothed_latents.csv").exists()
+
+
+def test_singleview_script_batches_videos(tmp_path):
+    """Two 'videos' (the mirror-mouse fixture and a copy with frames
+    reversed) smoothed in one batched call must equal the per-keypoint
+    single-view entry point on each."""
+    from eks_amd import io
+    from eks_amd.scripts import singleview_example
+    from eks_amd.singleview_smoother import ensemble_kalman_smoother_single_view
+    src = os.path.join(CSV, "mirror-mouse")
+    v2 = tmp_path / "video2"
+    v2.mkdir()
+    for f in sorted(os.listdir(src)):
+        df = io.read_dlc_csv(os.path.join(src, f))
+        df.iloc[::-1].set_axis(df.index).to_csv(v2 / f)
+    out = tmp_path / "out"
+    kps = ["paw1LH_top", "paw2LF_bot"]
+    singleview_example.main(["--csv-dir", src, str(v2), "--bodypart-list", *kps,
+                             "--save-dir", str(out)])
+    for vd, name in ((src, "mirror-mouse"), (str(v2), "video2")):
+        res = pd.read_csv(out / name / "eks.csv", header=[0, 1, 2], index_col=0)
+        ml, _, _ = io.load_markers_dir(vd)
+        for kp in kps:
+            ref = ensemble_kalman_smoother_single_view(ml, kp, 0.01, 25)["markers_df"]
+            a = res.loc[:, ("ensemble-kalman_tracker", kp, ["x", "y"])].to_numpy()
+            b = ref.to_numpy()[:, :2]
+            assert np.abs(a - b).max() < TOL
+        lik = res.loc[:, (slice(None), slice(None), "likelihood")].to_numpy()
+        assert (lik == 1.0).all()

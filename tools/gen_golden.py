@@ -316,8 +316,99 @@ def gen_newton(mv, ps, ut):
           golden_latents=g)
 
 
+def gen_cli(mv, ps, ut):
+    """Script-level fixtures (F1): the first 300 frames of the mirror-mouse and
+    ibl-pupil member CSVs (data lines copied verbatim) and the outputs the
+    reference's scripts produce on them (scripts/multicam_example.py,
+    scripts/pupil_example.py), with the reference functions the scripts call."""
+    import eks.newton_eks as ne
+    import eks.ensemble_kalman as ek
+    nrow = 300
+    base = os.path.join(OUT, "csv")
+    for ds in ("mirror-mouse", "ibl-pupil"):
+        os.makedirs(os.path.join(base, ds), exist_ok=True)
+        for f in sorted(glob.glob(os.path.join(REF, "data", ds, "*.csv"))):
+            lines = open(f).read().splitlines(True)
+            with open(os.path.join(base, ds, os.path.basename(f)), "w") as fo:
+                fo.writelines(lines[:3 + nrow])
+    exp = os.path.join(base, "expected")
+    os.makedirs(exp, exist_ok=True)
+
+    def load(ds):
+        ml, raw = [], None
+        for f in sorted(glob.glob(os.path.join(base, ds, "*.csv"))):
+            raw = pd.read_csv(f, header=[0, 1, 2], index_col=0)
+            kps = [c[1] for c in raw.columns[::3]]
+            ml.append(ut.convert_lp_dlc(raw, kps, model_name=raw.columns[0][0]))
+        return ml, raw, kps
+
+    # multicam_example.py (:96-160), both eks versions
+    ml, raw, _ = load("mirror-mouse")
+    cams = ["top", "bot"]
+    for version, fn, fname in (("standard", mv.ensemble_kalman_smoother_multi_cam, "eks.csv"),
+                               ("opti", mv.eks_opti_smoother_multi_cam, "eks_opti.csv")):
+        out = raw.copy()
+        out.columns = out.columns.set_levels(['ensemble-kalman_tracker'], level=0)
+        for col in out.columns:
+            out[col].values[:] = 1.0 if col[-1] == 'likelihood' else np.nan
+        for kp in ["paw1LH", "paw2LF", "paw3RF", "paw4RH"]:
+            by_cam = [[] for _ in cams]
+            for m in ml:
+                for c, cam in enumerate(cams):
+                    keys = [k for k in m.keys() if cam in k and 'likelihood' not in k and kp in k]
+                    by_cam[c].append(m[keys])
+            kw = dict(plot=False) if version == "opti" else {}
+            dfs = fn(by_cam, kp, 0.01, 25, cams, **kw)
+            for cam in cams:
+                for coord in ("x", "y"):
+                    out.loc[:, ('ensemble-kalman_tracker', f'{kp}_{cam}', coord)] = \
+                        dfs[f'{cam}_df'].loc[:, ('ensemble-kalman_tracker', kp, coord)]
+        out.to_csv(os.path.join(exp, fname))
+        print(f"  wrote expected/{fname}")
+    # pupil_example.py (:76-114), --diameter-s .99 --com-s .99
+    ml, raw, kps = load("ibl-pupil")
+    A = np.diag([0.99, 0.99, 0.99])
+    d = ps.ensemble_kalman_smoother_pupil(ml, kps, 'ensemble-kalman_tracker', A)
+    d['markers_df'].to_csv(os.path.join(exp, "kalman_smoothed_pupil_traces.csv"))
+    d['latents_df'].to_csv(os.path.join(exp, "kalman_smoothed_latents.csv"))
+    # opti: eks_opti_smoother_pupil's computation (its plot=False branch
+    # references an undefined q; see eks_amd.smoothers.eks_opti_smoother_pupil)
+    keys = ['pupil_top_r_x', 'pupil_top_r_y', 'pupil_bottom_r_x', 'pupil_bottom_r_y',
+            'pupil_right_r_x', 'pupil_right_r_y', 'pupil_left_r_x', 'pupil_left_r_y']
+    preds, ev, _, avg_d, _, _ = ek.ensemble(ml, keys)
+    loc = ps.get_pupil_location(avg_d)
+    diam = ps.get_pupil_diameter(avg_d)
+    mx, my = loc[:, 0].mean(), loc[:, 1].mean()
+    y = preds.copy()
+    y[:, 0::2] -= mx
+    y[:, 1::2] -= my
+    vx, vy, vd = np.var(loc[:, 0] - mx), np.var(loc[:, 1] - my), np.var(diam)
+    Bm = np.array([[0, 1, 0], [-.5, 0, 1], [0, 1, 0], [.5, 0, 1], [.5, 1, 0], [0, 0, 1],
+                   [-.5, 1, 0], [0, 0, 1]], dtype=np.float64)
+    q = ne.kalman_newton_recursive(y, np.array([diam.mean(), 0.0, 0.0]), np.diag([vd, vx, vy]), A,
+                                   Bm, ev, np.diag([vd, vx, vy]) * (1 - 0.99 ** 2))
+    mk = q @ Bm.T
+    mk[:, 0::2] += mx
+    mk[:, 1::2] += my
+    nan = np.full(len(q), np.nan)
+    cols = []
+    for kp in ('top', 'right', 'bottom', 'left'):
+        j = keys.index(f'pupil_{kp}_r_x')
+        cols += [mk[:, j], mk[:, j + 1], nan]
+    pd.DataFrame(np.stack(cols, 1), columns=ut.make_dlc_pandas_index(kps)).to_csv(
+        os.path.join(exp, "opti_eks_pupil_traces.csv"))
+    idx = pd.MultiIndex.from_arrays([['ensemble-kalman_tracker'] * 3,
+                                     ['diameter', 'com_x', 'com_y']], names=('scorer', 'latent'))
+    pd.DataFrame(np.stack([q[:, 0], q[:, 1] + mx, q[:, 2] + my], 1), columns=idx).to_csv(
+        os.path.join(exp, "opti_eks_latents.csv"))
+    print("  wrote expected pupil outputs")
+
+
 def main():
     ek, mv, ps, ut = _import_reference()
+    if len(sys.argv) > 1 and sys.argv[1] == "cli":
+        gen_cli(mv, ps, ut)
+        return
     if len(sys.argv) > 1 and sys.argv[1] == "newton":
         gen_newton(mv, ps, ut)
         return
@@ -328,6 +419,7 @@ def main():
     gen_fish(ut, mv)
     gen_pupil(ps, ut)
     gen_newton(mv, ps, ut)
+    gen_cli(mv, ps, ut)
 
 
 if __name__ == "__main__":
