@@ -118,17 +118,34 @@ def ensemble_dev(torch, obs_view, mode="median"):
     return preds, var
 
 
-def fit_singleview(torch, obs_view, s, q, chunk=2048):
-    """Per-trajectory single-view models, fitted on device in chunks."""
-    from eks_amd import batch, fit
-    parts = []
-    for lo in range(0, obs_view.shape[0], chunk):
-        preds, var = ensemble_dev(torch, obs_view[lo:lo + chunk])
-        m = fit.singleview_model_batch(preds, var, s, q)
-        parts.append(batch.pack_params(m["m0"], m["S0"], m["A"], m["Q"], m["C"], m["offset"],
-                                       device=obs_view.device))
-        del preds, var, m
-    return torch.cat(parts, dim=0).contiguous()
+def cpu_pipeline(stack, fit_fn, mode="median"):
+    """One trajectory through the CPU oracle, phases timed separately:
+    ensemble, model fit, forward + backward + projection.  Returns
+    (out, t_ensemble, t_fit, t_smooth)."""
+    import numpy as np
+    from oracle import eks_oracle as O
+    t0 = time.perf_counter()
+    preds, ev = O.ensemble_array(stack, mode)
+    t1 = time.perf_counter()
+    p = fit_fn(preds, ev)
+    t2 = time.perf_counter()
+    y = p["y"]
+    R = np.eye(y.shape[1])
+    mf, Vf, S = O.filtering_pass(y, p["m0"], p["S0"], p["C"], R, p["A"], p["Q"], ev)
+    ms, _, _ = O.smooth_backward(y, mf, Vf, S, p["A"])
+    out = ms @ p["C"].T + p["means"]
+    t3 = time.perf_counter()
+    return out, t1 - t0, t2 - t1, t3 - t2
+
+
+def cpu_result(units, outs_times, gpu_outs, sample):
+    """Hot-path rate (ensemble + filter + smoother + projection, the scope of
+    the GPU step) and end-to-end rate (plus the model fit) of the CPU runs."""
+    t_hot = sum(te + ts for _, te, _, ts in outs_times)
+    t_all = sum(te + tf + ts for _, te, tf, ts in outs_times)
+    diff = max(float(abs(o - g).max()) for (o, _, _, _), g in zip(outs_times, gpu_outs))
+    return dict(value=units / t_hot, e2e_value=units / t_all, dt=t_all, diff=diff,
+                sample=sample)
 
 
 # ---------------------------------------------------------------------------
@@ -148,7 +165,10 @@ def workload_singleview(torch, a, dev, rank, world, config):
     B = len(videos) * K
     obs_tm = gen_videos(torch, videos, K, E, T, a.seed, dev)          # (T, E, 2, B)
     obs = obs_tm.permute(3, 0, 1, 2)                                   # (B, T, E, 2) view
-    params = fit_singleview(torch, obs, a.smooth_param, a.quantile_keep)
+    fit_status = torch.empty((B,), dtype=torch.int32, device=dev)
+    fit_kw = dict(kind="singleview", n=2, r=2, smooth_param=a.smooth_param,
+                  quantile_keep=a.quantile_keep, status=fit_status)
+    params, _ = batch.fit(obs, **fit_kw)                               # eks_fit (F2)
     out = torch.empty((T, B, 2), dtype=torch.float64, device=dev).permute(1, 0, 2)
     status = torch.empty((B,), dtype=torch.int32, device=dev)
     flags = _lib.EKS_MODEL_A_IDENTITY | _lib.EKS_MODEL_C_IDENTITY  # single-view: A = C = I2
@@ -156,25 +176,27 @@ def workload_singleview(torch, a, dev, rank, world, config):
     def step():
         batch.smooth(obs, params, n=2, r=2, out=out, status=status, algo=a.algo, flags=flags)
 
+    def fit_step():
+        batch.fit(obs, params=params, check=False, **fit_kw)
+
     def cpu(n_traj):
         import numpy as np
         from oracle import eks_oracle as O
         host = obs_tm[:, :, :, :n_traj].cpu().numpy().astype(np.float64)  # (T, E, 2, b)
         gpu = out[:n_traj].cpu().numpy()
-        t0 = time.perf_counter()
-        outs = [O.singleview_smooth(np.ascontiguousarray(np.transpose(host[..., b], (1, 0, 2))),
-                                    a.smooth_param, a.quantile_keep)[0] for b in range(n_traj)]
-        dt = time.perf_counter() - t0
-        diff = max(float(np.abs(o - gpu[b]).max()) for b, o in enumerate(outs))
-        return n_traj * T / dt, dt, diff, (f"{n_traj} trajectories x {T} frames of this workload "
-                                           f"(oracle.singleview_smooth: ensemble + fit + filter + "
-                                           f"smoother, numpy, 1 thread)")
+        fit_fn = lambda p, v: O.singleview_params(p, v, a.smooth_param, a.quantile_keep)  # noqa
+        runs = [cpu_pipeline(np.ascontiguousarray(np.transpose(host[..., b], (1, 0, 2))), fit_fn)
+                for b in range(n_traj)]
+        return cpu_result(n_traj * T, runs, gpu,
+                          f"{n_traj} trajectories x {T} frames of this workload (oracle "
+                          f"ensemble + filtering_pass + smooth_backward + projection, numpy, "
+                          f"1 thread; the single-view fit timed separately for end_to_end)")
 
     desc = (f"config {config}: " + (f"batch of {a.videos} videos x " if config == 4 else "1 video x ")
             + f"{K} keypoints x {E} members x {T} frames, single-view EKS (ensemble median/var "
             f"-> forward KF -> RTS -> projection), float32 members, float64 recursions/outputs")
-    return dict(step=step, status=status, units=B * T, bytes_per_unit=E * 2 * 4 + 2 * 8,
-                cpu=cpu, cpu_default=24 if config == 4 else 2, desc=desc,
+    return dict(step=step, fit_step=fit_step, status=status, units=B * T,
+                bytes_per_unit=E * 2 * 4 + 2 * 8, cpu=cpu, cpu_default=24 if config == 4 else 2, desc=desc,
                 cfg=dict(videos=a.videos if config == 4 else 1, keypoints=K, members=E, frames=T,
                          trajectories_per_rank=B, smooth_param=a.smooth_param,
                          quantile_keep=a.quantile_keep),
@@ -193,38 +215,34 @@ def workload_multiview(torch, a, dev, rank, world):
     n = 2 * V
     obs_tm = torch.from_numpy(np.ascontiguousarray(st.transpose(1, 0, 3, 2))).to(dev)  # (T,E,8,K)
     obs = obs_tm.permute(3, 0, 1, 2)
-    preds, var = ensemble_dev(torch, obs)
-    preds, var = preds.cpu().numpy(), var.cpu().numpy()
-    models = [fit.multicam_model(preds[k], var[k], a.smooth_param, a.quantile_keep)
-              for k in range(K)]
-    stackp = lambda key: np.stack([m[key] for m in models])  # noqa: E731
-    params = batch.pack_params(stackp("m0"), stackp("S0"), stackp("A"), stackp("Q"), stackp("C"),
-                               stackp("offset"), device=dev)
-    flags = batch.model_flags(stackp("A"), stackp("C"))
+    fit_status = torch.empty((K,), dtype=torch.int32, device=dev)
+    fit_kw = dict(kind="multicam", n=n, r=3, smooth_param=a.smooth_param,
+                  quantile_keep=a.quantile_keep, status=fit_status)
+    params, _ = batch.fit(obs, **fit_kw)                               # eks_fit (F2): PCA model
+    flags = _lib.EKS_MODEL_A_IDENTITY                                  # A = I3 by construction
     out = torch.empty((T, K, n), dtype=torch.float64, device=dev).permute(1, 0, 2)
     status = torch.empty((K,), dtype=torch.int32, device=dev)
 
     def step():
         batch.smooth(obs, params, n=n, r=3, out=out, status=status, algo=a.algo, flags=flags)
 
+    def fit_step():
+        batch.fit(obs, params=params, check=False, **fit_kw)
+
     def cpu(n_traj):
         from oracle import eks_oracle as O
         gpu = out[:n_traj].cpu().numpy()
-        t0 = time.perf_counter()
-        outs = []
-        for k in range(n_traj):
-            cams = [st[:, :, k, 2 * c:2 * c + 2].astype(np.float64) for c in range(V)]
-            outs.append(O.multicam_smooth(cams, a.smooth_param, a.quantile_keep)[0])
-        dt = time.perf_counter() - t0
-        diff = max(float(np.abs(o - gpu[k]).max()) for k, o in enumerate(outs))
-        return n_traj * T / dt, dt, diff, (f"{n_traj} keypoints x {T} frames x {V} cameras of "
-                                           f"this workload (oracle.multicam_smooth, numpy, "
-                                           f"1 thread)")
+        fit_fn = lambda p, v: O.multicam_params(p, v, a.smooth_param, a.quantile_keep)  # noqa
+        runs = [cpu_pipeline(st[:, :, k, :].astype(np.float64), fit_fn) for k in range(n_traj)]
+        return cpu_result(n_traj * T, runs, gpu,
+                          f"{n_traj} keypoints x {T} frames x {V} cameras of this workload "
+                          f"(oracle ensemble + filtering_pass + smooth_backward + projection, "
+                          f"numpy, 1 thread; the PCA fit timed separately for end_to_end)")
 
     desc = (f"config 3: multiview PCA smoother, {V} cameras x {K} keypoints x {E} members x "
             f"{T} frames (r=3 latent, n=8), float32 members, float64 recursions/outputs")
-    return dict(step=step, status=status, units=K * T, bytes_per_unit=E * n * 4 + n * 8,
-                cpu=cpu, cpu_default=2, desc=desc,
+    return dict(step=step, fit_step=fit_step, status=status, units=K * T,
+                bytes_per_unit=E * n * 4 + n * 8, cpu=cpu, cpu_default=2, desc=desc,
                 cfg=dict(cameras=V, keypoints=K, members=E, frames=T,
                          smooth_param=a.smooth_param, quantile_keep=a.quantile_keep),
                 key=f"config3-multiview-k{K}-e{E}-t{T}-n{world}")
@@ -271,20 +289,16 @@ def workload_pupil(torch, a, dev, rank, world):
         Tc = min(T, 200000)  # bounded sample: the first Tc frames, chosen model
         b = int(state["best"].item())
         Ab = cands[b]["A"]
-        t0 = time.perf_counter()
-        mk, _, _, _ = O.pupil_smooth(st[:, :Tc].astype(np.float64), Ab)
-        dt = time.perf_counter() - t0
-        # the GPU reference for the same prefix and model
-        sub = obs[:, :Tc]
-        from eks_amd import fit as F
-        pre = F.pupil_model(O.ensemble_array(st[:, :Tc].astype(np.float64))[0], Ab)
+        run = cpu_pipeline(st[:, :Tc].astype(np.float64), lambda p, v: O.pupil_params(p, Ab))
+        # the GPU output for the same prefix and model
+        pre = fit.pupil_model(O.ensemble_array(st[:, :Tc].astype(np.float64))[0], Ab)
         pb = batch.pack_params(pre["m0"], pre["S0"], pre["A"], pre["Q"], pre["C"], pre["offset"],
                                device=dev)
-        g = batch.smooth(sub, pb, n=8, r=3)["out"][0].cpu().numpy()
-        diff = float(np.abs(g - mk).max())
-        return 4 * Tc / dt, dt, diff, (f"first {Tc} frames x 4 keypoints, best model "
-                                       f"(oracle.pupil_smooth, numpy, 1 thread); the GPU step "
-                                       f"also scores {len(cands)} candidate models")
+        g = batch.smooth(obs[:, :Tc], pb, n=8, r=3)["out"][0].cpu().numpy()
+        return cpu_result(4 * Tc, [run], [g],
+                          f"first {Tc} frames x 4 keypoints, best model (oracle ensemble + "
+                          f"filtering_pass + smooth_backward + projection, numpy, 1 thread); "
+                          f"the GPU step also scores {len(cands)} candidate models")
 
     desc = (f"config 5: IBL-pupil smoother, {T} frames x 4 keypoints x {E} members (r=3 latent, "
             f"n=8): NLL sweep over {len(cands)} (diameter_s, com_s) models (filter-only, "
@@ -357,6 +371,31 @@ def main():
     units_local = w["units"]
     units_total = dist.sum_over_ranks(units_local, device=dev)
 
+    # end to end: the model fit on the device (eks_fit) + the hot path, i.e.
+    # what the reference's per-keypoint wrappers do from member predictions
+    e2e = None
+    if "fit_step" in w:
+        fit_step = w["fit_step"]
+        for _ in range(max(1, a.warmup)):
+            fit_step()
+            step()
+        torch.cuda.synchronize()
+        dist.barrier()
+        f0 = time.perf_counter()
+        for _ in range(a.steps):
+            fit_step()
+            step()
+        torch.cuda.synchronize()
+        dist.barrier()
+        e2e_s = dist.max_over_ranks(time.perf_counter() - f0, device=dev)
+        _lib.profile_begin(4 * a.steps)
+        for _ in range(a.steps):
+            fit_step()
+        fit_kernels = [(n, ms / a.steps) for n, ms in _lib.profile_end()]
+        e2e = dict(value=units_total / e2e_s * a.steps, ms_per_step=e2e_s / a.steps * 1e3,
+                   fit_kernels_ms={n: round(ms, 4) for n, ms in fit_kernels},
+                   scope="eks_fit (ensemble, good-frame percentile, model fit) + eks_smooth")
+
     gather_ms = None
     if a.gather and world > 1 and a.config == 4:
         torch.cuda.synchronize()
@@ -373,11 +412,13 @@ def main():
     cpu = None
     maxdiff = None
     n_cpu = w["cpu_default"] if a.cpu_sample is None else a.cpu_sample
+    cpu_e2e = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline and n_cpu > 0:
         with threadpool_limits(1):
-            v, dt, maxdiff, sample = w["cpu"](n_cpu)
-        cpu = dict(value=v, unit="kp-ts/s", cores=1, kind="port",
-                   sample=f"{sample}, {dt:.1f} s")
+            c = w["cpu"](n_cpu)
+        maxdiff, cpu_e2e = c["diff"], c["e2e_value"]
+        cpu = dict(value=c["value"], unit="kp-ts/s", cores=1, kind="port",
+                   sample=f"{c['sample']}, {c['dt']:.1f} s")
 
     if rank == 0:
         value = units_total / elapsed_max * a.steps
@@ -415,6 +456,7 @@ def main():
             },
             "cpu_baseline": cpu,
             "max_abs_diff_vs_cpu": maxdiff,
+            "end_to_end": None if e2e is None else dict(e2e, cpu_value=cpu_e2e),
             "setup_s": round(setup_s, 2),
         }
         if "extra" in w:

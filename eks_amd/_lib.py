@@ -18,6 +18,7 @@ HEADERS = [HEADER, os.path.join(os.path.dirname(HERE), "include", "eks_io.h")]
 EKS_OK, EKS_ERR_ARG, EKS_ERR_UNSUPPORTED, EKS_ERR_HIP = 0, 1, 2, 4
 EKS_STATUS_SINGULAR, EKS_STATUS_BAD_MODEL, EKS_STATUS_SCAN = 1, 2, 4
 EKS_MODEL_A_IDENTITY, EKS_MODEL_C_IDENTITY = 1, 2
+EKS_FIT_SINGLEVIEW, EKS_FIT_MULTICAM = 1, 2
 EKS_F32, EKS_F64 = 0, 1
 EKS_MEDIAN, EKS_MEAN = 0, 1
 
@@ -46,6 +47,9 @@ SIGNATURES = {
     "eks_smooth_chunk_len": (_i64, [_i64, _i64, _i32]),
     "eks_newton_filter": (_i32, [_i64, _i64, _i32, _i32, _p, _p, _p, _p, _p, _p, _p, _i32, _i32,
                                  _p, _p, _p]),
+    "eks_fit_workspace_bytes": (_sz, [_i64, _i64, _i32]),
+    "eks_fit": (_i32, [_p, _i32, _i64, _i64, _i32, _i32, _i32, _i64, _i64, _i64, _i64, _i32, _i32,
+                       C.c_double, C.c_double, _p, _p, _sz, _p, _p]),
     "eks_profile_begin": (_i32, [_i32]),
     # include/eks_io.h (host-only)
     "eks_io_last_error": (C.c_char_p, []),

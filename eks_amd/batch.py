@@ -51,10 +51,12 @@ def pack_params(m0, S0, A, Q, C, offset, device="cuda"):  # noqa: C901
     return out
 
 
-def workspace(nbytes: int, device=None):
+def workspace(nbytes: int, device=None, slot: str = "smooth"):
+    """Cached device scratch buffer per (device, slot); reused by later calls
+    on the same stream (the kernels are stream-ordered)."""
     import torch
     dev = torch.device("cuda") if device is None else torch.device(device)
-    key = (dev.index if dev.index is not None else torch.cuda.current_device())
+    key = (dev.index if dev.index is not None else torch.cuda.current_device(), slot)
     buf = _WS.get(key)
     if buf is None or buf.numel() < nbytes:
         buf = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=dev)
@@ -139,6 +141,44 @@ def smooth(obs, params, *, n: int, r: int, mode: str = "median", out=None, want_
         if st_all & _lib.EKS_STATUS_SINGULAR:
             raise np.linalg.LinAlgError("Singular matrix")
     return res
+
+
+def fit(obs, *, kind: str, n: int, r: int, smooth_param: float, quantile_keep: float,
+        mode: str = "median", check: bool = True, params=None, status=None):
+    """Batched model fit on the device (eks_fit, F2): (B, T, E, n) member view
+    -> (B, eks_param_len(n, r)) float64 parameter rows for ``smooth``.
+
+    kind "singleview" (r == n) or "multicam" (PCA with r
+    axes; eks/multiview_pca_smoother.py:684-731)."""
+    torch = _lib.require_gpu()
+    if obs.dim() != 4 or obs.shape[3] != n:
+        raise ValueError("obs must be viewed as (B, T, E, n)")
+    B, T, E, _ = obs.shape
+    dt = _lib.EKS_F32 if obs.dtype == torch.float32 else _lib.EKS_F64
+    if obs.dtype not in (torch.float32, torch.float64):
+        raise TypeError("obs must be float32 or float64")
+    if mode not in ("median", "mean"):
+        raise ValueError(f"{mode} averaging not supported")
+    k = {"singleview": _lib.EKS_FIT_SINGLEVIEW, "multicam": _lib.EKS_FIT_MULTICAM}[kind]
+    lib = _lib.load()
+    if params is None:
+        params = torch.empty((B, param_len(n, r)), dtype=torch.float64, device=obs.device)
+    elif params.shape != (B, param_len(n, r)) or params.dtype != torch.float64 \
+            or not params.is_contiguous():
+        raise ValueError(f"params must be a contiguous ({B}, {param_len(n, r)}) float64 tensor")
+    if status is None:
+        status = torch.empty((B,), dtype=torch.int32, device=obs.device)
+    ws = workspace(lib.eks_fit_workspace_bytes(B, T, n), obs.device, slot="fit")
+    sb, st, se, sj = obs.stride()
+    _lib.check(lib.eks_fit(obs.data_ptr(), dt, B, T, E, n, r, sb, st, se, sj,
+                           _lib.EKS_MEDIAN if mode == "median" else _lib.EKS_MEAN, k,
+                           float(smooth_param), float(quantile_keep), params.data_ptr(),
+                           ws.data_ptr(), ws.numel(), status.data_ptr(), _lib.stream_ptr()),
+               "eks_fit")
+    if check and bool((status != 0).any()):
+        raise ValueError("eks_fit: no frame passed the variance threshold (NaN ensemble "
+                         "variances?)")
+    return params, status
 
 
 def nll(obs, params, *, n: int, r: int, mode: str = "median", flags: int = 0, algo: int = 0,

@@ -1,0 +1,773 @@
+// F2: batched model fit on the device -- the step before the smoother.
+//
+// Replaces the per-keypoint host fit of
+//   eks/multiview_pca_smoother.py:684-731   (multi-camera PCA model)
+//   SURVEY.md §8 A6                         (single-view model, same template
+//                                            without the PCA)
+// for B trajectories at once:
+//   good   = frames whose max_j ensemble variance <= np.percentile(., q)
+//   offset = mean of the good ensemble predictions            (:698-700)
+//   single-view: S0 = diag(var(good y)), Q = s cov(diff(good y)), A = C = I
+//   multicam:    W = top-r principal axes of the good y       (:708)
+//                S0 = diag(var(good y W^T)), Q = s W cov(diff(good y)) W^T,
+//                A = I, C = W^T                               (:722-730)
+// written straight into the packed parameter rows eks_smooth reads.
+//
+// Kernels (all f64):
+//   k_fit_worst   one lane per (trajectory, chunk of frames): ensemble of
+//                 every frame (same code as eks_ensemble), v_t = max_j var
+//                 stored trajectory-major
+//   k_fit_select  one 256-thread block per trajectory: exact order
+//                 statistics v_(lo), v_(lo+1) by MSD radix select on the
+//                 IEEE bit patterns (12-bit digits, LDS histograms, early
+//                 exit once the candidate is unique), then numpy's linear
+//                 interpolation -> threshold
+//   k_fit_accum   one lane per (trajectory, chunk): ensemble again, keep
+//                 frames with v_t <= threshold, chunk statistics of y and of
+//                 the differences between consecutive kept frames (shifted
+//                 sums -> mean / scatter matrix), first / last kept y
+//   k_fit_final   one lane per trajectory: merge the chunks in order (Chan
+//                 et al. pairwise update; the kept-frame pair straddling
+//                 two chunks is added here), PCA by cyclic Jacobi on the
+//                 n x n scatter matrix, parameter rows
+// The results agree with the numpy fit to rounding (different summation
+// order), which moves the smoothed outputs by ~1e-12 px.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+
+#include "../../include/eks_hip.h"
+#include "eks_common.hpp"
+#include "ensemble.hpp"
+
+namespace eks {
+
+namespace {
+
+constexpr int kDigitBits = 12;
+constexpr int kBins = 1 << kDigitBits;
+
+// ensemble of one frame: y[j] = median/mean, v = max_j var (NaN-propagating
+// like np.max)
+template <int E, int N, typename T>
+EKS_DEV void frame_ensemble(const T *p, long long se, long long sj, int Ert, bool median,
+                            double (&y)[N], double &v) {
+  v = -1.0;
+  bool nan = false;
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    double avg, var;
+    if constexpr (E > 0) {
+      T raw[E];
+#pragma unroll
+      for (int e = 0; e < E; ++e) raw[e] = p[j * sj + e * se];
+      ensemble_reduce<E, T>(raw, median, avg, var);
+    } else {
+      ensemble_reduce_rt<T>(p + j * sj, se, Ert, median, avg, var);
+    }
+    y[j] = avg;
+    nan |= (var != var);
+    v = var > v ? var : v;
+  }
+  if (nan) v = __builtin_nan("");
+}
+
+struct FitShape {
+  long long B, T;
+  int NC;          // chunks per trajectory
+  long long Lc;    // frames per chunk
+};
+
+constexpr int kTile = 16;  // frames per register tile: one 128-byte row segment per lane
+
+template <int E, int N, typename T>
+__global__ __launch_bounds__(256) void k_fit_worst(const T *__restrict__ obs, FitShape sh,
+                                                   long long sb, long long st, long long se,
+                                                   long long sj, int Ert, int median,
+                                                   double *__restrict__ worst) {
+  // each lane computes kTile consecutive frames of its (trajectory, chunk)
+  // into LDS; the block then writes the trajectory-major rows as whole
+  // 128-byte segments (16 lanes per segment) instead of one 8-byte store
+  // per lane per frame
+  __shared__ double tile[256][kTile + 1];
+  __shared__ long long base[256];
+  const long long lane = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  const bool active = lane < sh.B * sh.NC;
+  long long b = 0, t0 = 0, t1 = 0;
+  if (active) {
+    b = lane % sh.B;
+    t0 = (lane / sh.B) * sh.Lc;
+    t1 = t0 + sh.Lc < sh.T ? t0 + sh.Lc : sh.T;
+  }
+  const T *pb = obs + b * sb;
+  const long long ntiles = sh.Lc / kTile;  // Lc is a multiple of kTile
+  for (long long kt = 0; kt < ntiles; ++kt) {
+    const long long t = t0 + kt * kTile;
+    if (active && t + kTile <= t1) {
+#pragma unroll
+      for (int k = 0; k < kTile; ++k) {
+        double y[N];
+        frame_ensemble<E, N, T>(pb + (t + k) * st, se, sj, Ert, median != 0, y,
+                                tile[threadIdx.x][k]);
+      }
+      base[threadIdx.x] = b * sh.T + t;
+    } else {
+      base[threadIdx.x] = -1;
+      if (active)
+        for (long long u = t; u < t1; ++u) {  // ragged end of the last chunk
+          double y[N], v;
+          frame_ensemble<E, N, T>(pb + u * st, se, sj, Ert, median != 0, y, v);
+          worst[b * sh.T + u] = v;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int p = 0; p < 256 / 16; ++p) {
+      const int r = p * 16 + (threadIdx.x >> 4), k = threadIdx.x & 15;
+      const long long o = base[r];
+      if (o >= 0) worst[o + k] = tile[r][k];
+    }
+    __syncthreads();
+  }
+}
+
+// Apply f to every key of a row, BLK threads, 8 independent loads in flight
+// per thread (memory-level parallelism for the global-memory passes)
+template <int BLK, typename F>
+EKS_DEV void for_keys(const uint64_t *keys, long long n, F &&f) {
+  constexpr int U = 8;
+  long long i = threadIdx.x;
+  for (; i + (U - 1) * BLK < n; i += U * BLK) {
+    uint64_t x[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) x[u] = keys[i + u * BLK];
+#pragma unroll
+    for (int u = 0; u < U; ++u) f(x[u]);
+  }
+  for (; i < n; i += BLK) f(keys[i]);
+}
+
+// block-wide exclusive prefix sum of one value per thread (BLK threads)
+template <int BLK>
+EKS_DEV long long block_excl_scan(long long x, long long *tmp, long long &total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  long long inc = x;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const long long y = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += y;
+  }
+  if (lane == 63) tmp[wave] = inc;
+  __syncthreads();
+  long long base = 0, tot = 0;
+  for (int w = 0; w < BLK / 64; ++w) {
+    base += w < wave ? tmp[w] : 0;
+    tot += tmp[w];
+  }
+  __syncthreads();
+  total = tot;
+  return base + inc - x;
+}
+
+// k-th smallest (0-based) key of the row, MSD radix select over the bits
+// below `top` (the keys' common prefix above it is `prefix`).  All threads
+// call it and get the same result.
+template <int BLK>
+EKS_DEV uint64_t block_select(const uint64_t *keys, long long n, long long k, int top,
+                              uint64_t prefix, unsigned *hist, uint64_t *su, long long *si) {
+  uint64_t mask = top >= 63 ? 0ull : ~((2ull << top) - 1);  // bits above `top` fixed
+  for (int hi_bit = top; hi_bit >= 0; hi_bit -= kDigitBits) {
+    const int lo_bit = hi_bit - kDigitBits + 1 > 0 ? hi_bit - kDigitBits + 1 : 0;
+    const int bits = hi_bit - lo_bit + 1;
+    const unsigned nb = 1u << bits;
+    for (unsigned i = threadIdx.x; i < nb; i += blockDim.x) hist[i] = 0;
+    __syncthreads();
+    for_keys<BLK>(keys, n, [&](uint64_t x) {
+      if ((x & mask) == prefix) atomicAdd(&hist[(x >> lo_bit) & (nb - 1)], 1u);
+    });
+    __syncthreads();
+    // parallel scan of the histogram: thread i owns bins [i*per, (i+1)*per)
+    const unsigned per = (nb + BLK - 1) / BLK;
+    long long mine = 0;
+    for (unsigned d = threadIdx.x * per; d < (threadIdx.x + 1) * per && d < nb; ++d)
+      mine += hist[d];
+    long long total;
+    long long acc = block_excl_scan<BLK>(mine, si + 2, total);
+    if (k >= acc && k < acc + mine) {  // exactly one thread
+      unsigned d = threadIdx.x * per;
+      while (acc + hist[d] <= k) acc += hist[d++];
+      su[0] = prefix | ((uint64_t)d << lo_bit);
+      si[0] = k - acc;
+      si[1] = hist[d];
+    }
+    __syncthreads();
+    prefix = su[0];
+    k = si[0];
+    const long long left = si[1];
+    mask |= (uint64_t)(nb - 1) << lo_bit;
+    __syncthreads();
+    if (left == 1 && lo_bit > 0) {  // the candidate is unique: find it
+      if (threadIdx.x == 0) su[1] = ~0ull;
+      __syncthreads();
+      for_keys<BLK>(keys, n, [&](uint64_t x) {
+        if ((x & mask) == prefix) atomicMin((unsigned long long *)&su[1], x);
+      });
+      __syncthreads();
+      const uint64_t r = su[1];
+      __syncthreads();
+      return r;
+    }
+  }
+  return prefix;
+}
+
+// One block per trajectory.  Pass 1 histograms the top digit (bits 51-62:
+// exponent and first mantissa bit; variances are >= 0 so bit patterns sort
+// like values) over the row in global memory; pass 2 compacts the keys of
+// the bin holding rank `lo` into LDS; the remaining digits and the
+// neighbouring order statistic are then resolved in LDS.  A bin larger than
+// the LDS buffer falls back to selecting over the global row.
+constexpr int kCand = 4096;  // LDS candidates (32 KB): three blocks per CU
+
+template <int BLK>
+__global__ __launch_bounds__(BLK) void k_fit_select(const double *__restrict__ worst,
+                                                    long long TT, long long lo, long long hi,
+                                                    double g, double *__restrict__ thr) {
+  __shared__ unsigned hist[kBins];
+  __shared__ uint64_t cand[kCand];
+  __shared__ uint64_t su[4];
+  __shared__ long long si[2 + BLK / 64];
+  __shared__ unsigned ncand;
+  __shared__ int any_nan;
+  const long long b = blockIdx.x;
+  const uint64_t *keys = reinterpret_cast<const uint64_t *>(worst + b * TT);
+  constexpr int lo_bit = 51;
+  for (unsigned i = threadIdx.x; i < kBins; i += BLK) hist[i] = 0;
+  if (threadIdx.x == 0) {
+    any_nan = 0;
+    ncand = 0;
+  }
+  __syncthreads();
+  // pass 1: NaN check + top-digit histogram
+  bool nan = false;
+  for_keys<BLK>(keys, TT, [&](uint64_t x) {
+    nan |= (x & 0x7fffffffffffffffull) > 0x7ff0000000000000ull;
+    atomicAdd(&hist[(x >> lo_bit) & (kBins - 1)], 1u);
+  });
+  if (nan) any_nan = 1;
+  __syncthreads();
+  if (any_nan) {  // np.percentile of an array holding NaN is NaN: no frame kept
+    if (threadIdx.x == 0) thr[b] = __builtin_nan("");
+    return;
+  }
+  // bin of rank lo (parallel scan over the histogram)
+  {
+    constexpr unsigned per = kBins / BLK;
+    long long mine = 0;
+    for (unsigned d = threadIdx.x * per; d < (threadIdx.x + 1) * per; ++d) mine += hist[d];
+    long long total;
+    long long acc = block_excl_scan<BLK>(mine, si + 2, total);
+    if (lo >= acc && lo < acc + mine) {
+      unsigned d = threadIdx.x * per;
+      while (acc + hist[d] <= lo) acc += hist[d++];
+      su[0] = (uint64_t)d << lo_bit;
+      si[0] = lo - acc;
+      si[1] = hist[d];
+    }
+    __syncthreads();
+  }
+  const uint64_t binpfx = su[0];
+  const long long kin = si[0], cnt_bin = si[1];
+  const uint64_t binmask = ~((1ull << lo_bit) - 1);
+  __syncthreads();
+  uint64_t ka;
+  long long le_in_bin = -1;  // keys of the bin <= ka (when resolved in LDS)
+  uint64_t above_in_bin = ~0ull;
+  if (cnt_bin <= kCand) {
+    // pass 2: compact the bin into LDS
+    // wave-aggregated slot allocation: one LDS atomic per wave and key batch
+    for_keys<BLK>(keys, TT, [&](uint64_t x) {
+      const bool in = (x & binmask) == binpfx;
+      const uint64_t m = __ballot(in);
+      if (m == 0) return;
+      const int lane = threadIdx.x & 63;
+      const unsigned below = (unsigned)__popcll(m & ((1ull << lane) - 1));
+      unsigned base = 0;
+      if (lane == __ffsll((long long)m) - 1) base = atomicAdd(&ncand, (unsigned)__popcll(m));
+      base = __shfl(base, __ffsll((long long)m) - 1, 64);
+      if (in) cand[base + below] = x;
+    });
+    __syncthreads();
+    ka = block_select<BLK>(cand, cnt_bin, kin, lo_bit - 1, binpfx, hist, su, si);
+    if (hi != lo) {
+      if (threadIdx.x == 0) {
+        su[1] = ~0ull;
+        si[0] = 0;
+      }
+      __syncthreads();
+      unsigned long long c = 0, ab = ~0ull;
+      for (long long i = threadIdx.x; i < cnt_bin; i += BLK) {
+        const uint64_t x = cand[i];
+        c += x <= ka;
+        if (x > ka && x < ab) ab = x;
+      }
+      atomicAdd((unsigned long long *)&si[0], c);
+      atomicMin((unsigned long long *)&su[1], ab);
+      __syncthreads();
+      le_in_bin = si[0];
+      above_in_bin = su[1];
+      __syncthreads();
+    }
+  } else {
+    ka = block_select<BLK>(keys, TT, lo, 62, 0ull, hist, su, si);
+  }
+  uint64_t kb = ka;
+  if (hi != lo) {
+    if (le_in_bin >= 0 && le_in_bin >= kin + 2) {
+      kb = ka;                      // ka repeats at rank lo + 1
+    } else if (le_in_bin >= 0 && above_in_bin != ~0ull) {
+      kb = above_in_bin;            // next key of the same bin
+    } else {
+      // rank lo + 1 lies above ka: v_(lo+1) = ka if ka repeats, else the least
+      // key above ka (one pass over the global row)
+      if (threadIdx.x == 0) {
+        su[1] = ~0ull;
+        si[0] = 0;
+      }
+      __syncthreads();
+      unsigned long long c = 0, ab = ~0ull;
+      for_keys<BLK>(keys, TT, [&](uint64_t x) {
+        c += x <= ka;
+        if (x > ka && x < ab) ab = x;
+      });
+      atomicAdd((unsigned long long *)&si[0], c);
+      atomicMin((unsigned long long *)&su[1], ab);
+      __syncthreads();
+      kb = si[0] >= hi + 1 ? ka : su[1];
+    }
+  }
+  if (threadIdx.x == 0) {
+    const double a = __longlong_as_double((long long)ka);
+    const double bb = __longlong_as_double((long long)kb);
+    const double d = bb - a;  // numpy's _lerp
+    thr[b] = g >= 0.5 ? bb - d * (1.0 - g) : a + d * g;
+  }
+}
+
+// per-chunk statistics, packed symmetric matrices (upper triangle, row-major)
+template <int N>
+struct ChunkStats {
+  static constexpr int kTri = N * (N + 1) / 2;
+  // [cnt | mean N | M2 tri | npair | dmean N | dM2 tri | first N | last N]
+  static constexpr int cnt = 0, mean = 1, M = 1 + N;
+  static constexpr int npair = 1 + N + kTri, dmean = npair + 1, dM = dmean + N;
+  static constexpr int first = dM + kTri, last = first + N;
+  static constexpr int kLen = last + N;
+};
+
+template <int N>
+EKS_DEV constexpr int tri(int i, int j) {  // i <= j
+  return i * N - i * (i - 1) / 2 + (j - i);
+}
+
+template <int E, int N, typename T>
+__global__ __launch_bounds__(256) void k_fit_accum(const T *__restrict__ obs, FitShape sh,
+                                                   long long sb, long long st, long long se,
+                                                   long long sj, int Ert, int median,
+                                                   const double *__restrict__ thr,
+                                                   double *__restrict__ part) {
+  using CS = ChunkStats<N>;
+  const long long lane = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (lane >= sh.B * sh.NC) return;
+  const long long b = lane % sh.B, c = lane / sh.B;
+  const long long t0 = c * sh.Lc, t1 = t0 + sh.Lc < sh.T ? t0 + sh.Lc : sh.T;
+  const T *pb = obs + b * sb;
+  const double th = thr[b];
+  // shifted sums: y relative to the chunk's first kept frame K
+  double K[N], S1[N], S2[CS::kTri], D1[N], D2[CS::kTri], last[N];
+  double cnt = 0.0, npair = 0.0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) K[i] = S1[i] = D1[i] = last[i] = 0.0;
+#pragma unroll
+  for (int i = 0; i < CS::kTri; ++i) S2[i] = D2[i] = 0.0;
+  for (long long t = t0; t < t1; ++t) {
+    double y[N], v;
+    frame_ensemble<E, N, T>(pb + t * st, se, sj, Ert, median != 0, y, v);
+    if (!(v <= th)) continue;
+    if (cnt == 0.0) {
+#pragma unroll
+      for (int i = 0; i < N; ++i) K[i] = y[i];
+    } else {
+      double d[N];
+#pragma unroll
+      for (int i = 0; i < N; ++i) d[i] = y[i] - last[i];
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        D1[i] += d[i];
+#pragma unroll
+        for (int j = i; j < N; ++j) D2[tri<N>(i, j)] = fma(d[i], d[j], D2[tri<N>(i, j)]);
+      }
+      npair += 1.0;
+    }
+    double z[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      z[i] = y[i] - K[i];
+      last[i] = y[i];
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      S1[i] += z[i];
+#pragma unroll
+      for (int j = i; j < N; ++j) S2[tri<N>(i, j)] = fma(z[i], z[j], S2[tri<N>(i, j)]);
+    }
+    cnt += 1.0;
+  }
+  double *o = part + lane * (long long)CS::kLen;
+  const double ic = cnt > 0.0 ? 1.0 / cnt : 0.0;
+  const double ip = npair > 0.0 ? 1.0 / npair : 0.0;
+  o[CS::cnt] = cnt;
+  o[CS::npair] = npair;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    o[CS::mean + i] = K[i] + S1[i] * ic;
+    o[CS::dmean + i] = D1[i] * ip;
+    o[CS::first + i] = K[i];
+    o[CS::last + i] = last[i];
+#pragma unroll
+    for (int j = i; j < N; ++j) {
+      o[CS::M + tri<N>(i, j)] = S2[tri<N>(i, j)] - S1[i] * S1[j] * ic;
+      o[CS::dM + tri<N>(i, j)] = D2[tri<N>(i, j)] - D1[i] * D1[j] * ip;
+    }
+  }
+}
+
+// Merge F consecutive chunk partials of one trajectory into one, in order
+// (Chan, Golub & LeVeque pairwise update; the kept pair straddling two
+// chunks is added as a one-sample difference).  One thread per (trajectory,
+// group, packed matrix element); every thread recomputes the counts and the
+// means it needs, so there is no cross-thread dependence.
+template <int N>
+__global__ __launch_bounds__(256) void k_fit_merge(long long B, int nc_in, int F,
+                                                   const double *__restrict__ in,
+                                                   double *__restrict__ out) {
+  using CS = ChunkStats<N>;
+  const int nc_out = (nc_in + F - 1) / F;
+  const long long gid = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  const long long total = B * nc_out * CS::kTri;
+  if (gid >= total) return;
+  const int e = (int)(gid % CS::kTri);
+  const long long bg = gid / CS::kTri;
+  const long long b = bg % B, g = bg / B;
+  int i = 0;
+  while (tri<N>(i, N - 1) < e) ++i;  // element e = (i, j), i <= j
+  const int j = i + (e - tri<N>(i, i));
+  double n = 0.0, mi = 0.0, mj = 0.0, Mij = 0.0;
+  double np_ = 0.0, di = 0.0, dj = 0.0, Dij = 0.0;
+  double fi = 0.0, fj = 0.0, li = 0.0, lj = 0.0;
+  bool have = false;
+  const int c0 = (int)g * F, c1 = c0 + F < nc_in ? c0 + F : nc_in;
+  for (int c = c0; c < c1; ++c) {
+    const double *o = in + ((long long)c * B + b) * CS::kLen;
+    const double cnt = o[CS::cnt];
+    if (cnt == 0.0) continue;
+    if (have) {  // pair (last kept of the previous chunks, first kept of this one)
+      const double xi = o[CS::first + i] - li, xj = o[CS::first + j] - lj;
+      const double nn = np_ + 1.0, f = np_ / nn;
+      Dij += (xi - di) * (xj - dj) * f;
+      di += (xi - di) / nn;
+      dj += (xj - dj) / nn;
+      np_ = nn;
+    } else {
+      fi = o[CS::first + i];
+      fj = o[CS::first + j];
+    }
+    {
+      const double nb = cnt, nn = n + nb, f = n * nb / nn;
+      const double dli = o[CS::mean + i] - mi, dlj = o[CS::mean + j] - mj;
+      Mij += o[CS::M + e] + dli * dlj * f;
+      mi += dli * (nb / nn);
+      mj += dlj * (nb / nn);
+      n = nn;
+    }
+    const double npb = o[CS::npair];
+    if (npb > 0.0) {
+      const double nn = np_ + npb, f = np_ * npb / nn;
+      const double dli = o[CS::dmean + i] - di, dlj = o[CS::dmean + j] - dj;
+      Dij += o[CS::dM + e] + dli * dlj * f;
+      di += dli * (npb / nn);
+      dj += dlj * (npb / nn);
+      np_ = nn;
+    }
+    li = o[CS::last + i];
+    lj = o[CS::last + j];
+    have = true;
+  }
+  double *w = out + ((long long)g * B + b) * CS::kLen;
+  w[CS::M + e] = Mij;
+  w[CS::dM + e] = Dij;
+  if (i == j) {
+    w[CS::mean + i] = mi;
+    w[CS::dmean + i] = di;
+    w[CS::first + i] = fi;
+    w[CS::last + i] = li;
+  }
+  if (e == 0) {
+    w[CS::cnt] = n;
+    w[CS::npair] = np_;
+  }
+}
+
+// Parameter rows from the fully merged statistics (one partial per
+// trajectory): one wavefront per trajectory, lane L = i N + j owning entry
+// (i, j) of the n x n matrices.  The PCA axes come from a cyclic Jacobi
+// eigen-decomposition done across the wave: each rotation is three
+// broadcasts and two lane shuffles, no matrix leaves the registers.
+template <int R, int N>
+__global__ __launch_bounds__(64) void k_fit_final(long long B, const double *__restrict__ part,
+                                                  int kind, double smooth_param,
+                                                  double *__restrict__ params,
+                                                  int32_t *__restrict__ status) {
+  using CS = ChunkStats<N>;
+  __shared__ double sV[N * N], sM[N * N], sD[N * N], sEv[N];
+  const long long b = blockIdx.x;
+  const int L = threadIdx.x;
+  const int i = L / N, j = L % N;
+  const bool own = L < N * N;
+  const double *o = part + b * CS::kLen;
+  const double n = o[CS::cnt];
+  double np_ = o[CS::npair];
+  if (np_ < 1.0) np_ = __builtin_nan("");  // np.cov of no pairs is NaN
+  const int ti = own ? (i <= j ? tri<N>(i, j) : tri<N>(j, i)) : 0;
+  const double Mij = own ? o[CS::M + ti] : 0.0;   // good-frame scatter matrix
+  const double Dij = own ? o[CS::dM + ti] : 0.0;  // difference scatter matrix
+  ParamLayout<R, N> P;
+  double *pr = params + b * (long long)P.len;
+  if (L < R) pr[P.m0 + L] = 0.0;
+  if (L < R * R) pr[P.A + L] = (L / R == L % R) ? 1.0 : 0.0;
+  if (L < N) pr[P.off + L] = o[CS::mean + L];
+  if (kind == EKS_FIT_SINGLEVIEW) {
+    // S0 = diag(var(good y)) (ddof 0), Q = s cov(diff) (ddof 1), A = C = I
+    if (own && i < R && j < R) {
+      pr[P.S0 + i * R + j] = i == j ? Mij / n : 0.0;
+      pr[P.Q + i * R + j] = smooth_param * (Dij / (np_ - 1.0));
+    }
+    if (own && j < R) pr[P.C + i * R + j] = i == j ? 1.0 : 0.0;
+  } else {
+    // principal axes of the good-frame scatter matrix (sklearn's PCA axes
+    // up to sign; outputs do not depend on the sign)
+    double a = Mij, v = (own && i == j) ? 1.0 : 0.0;
+    for (int sweep = 0; sweep < 60; ++sweep) {
+      double off = (own && i < j) ? a * a : 0.0, dia = (own && i == j) ? a * a : 0.0;
+#pragma unroll
+      for (int w = 32; w >= 1; w >>= 1) {
+        off += __shfl_xor(off, w, 64);
+        dia += __shfl_xor(dia, w, 64);
+      }
+      if (off == 0.0 || off <= 1e-34 * dia) break;
+      for (int p = 0; p < N - 1; ++p)
+        for (int q = p + 1; q < N; ++q) {
+          const double apq = __shfl(a, p * N + q, 64);
+          if (apq == 0.0) continue;  // wave-uniform
+          const double app = __shfl(a, p * N + p, 64), aqq = __shfl(a, q * N + q, 64);
+          const double theta = (aqq - app) / (2.0 * apq);
+          const double t = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+          const double c = 1.0 / sqrt(t * t + 1.0), sn = t * c;
+          // columns p, q:  a_ip' = c a_ip - s a_iq ; a_iq' = s a_ip + c a_iq  (same for V)
+          const int cp = (j == p) ? i * N + q : (j == q) ? i * N + p : L;
+          const double ao = __shfl(a, cp, 64), vo = __shfl(v, cp, 64);
+          if (own && j == p) {
+            a = c * a - sn * ao;
+            v = c * v - sn * vo;
+          } else if (own && j == q) {
+            a = sn * ao + c * a;
+            v = sn * vo + c * v;
+          }
+          // rows p, q:  a_pj'' = c a_pj' - s a_qj' ; a_qj'' = s a_pj' + c a_qj'
+          const int rp = (i == p) ? q * N + j : (i == q) ? p * N + j : L;
+          const double ar = __shfl(a, rp, 64);
+          if (own && i == p)
+            a = c * a - sn * ar;
+          else if (own && i == q)
+            a = sn * ar + c * a;
+        }
+    }
+    if (own) {
+      sV[L] = v;
+      sM[L] = Mij;
+      sD[L] = Dij;
+      if (i == j) sEv[i] = a;
+    }
+    __syncthreads();
+    // lane (k, l) < R x R: S0 = diag(W (M / n) W^T), Q = s W (DM / (np - 1)) W^T
+    // with W's rows the eigenvectors of the R largest eigenvalues
+    int order[R];
+    unsigned used = 0;
+#pragma unroll
+    for (int k = 0; k < R; ++k) {  // k-th largest eigenvalue (first index on ties)
+      int best = -1;
+      for (int e = 0; e < N; ++e)
+        if (!((used >> e) & 1u) && (best < 0 || sEv[e] > sEv[best])) best = e;
+      order[k] = best;
+      used |= 1u << best;
+    }
+    if (L < R * R) {
+      const int k = L / R, l = L % R;
+      int ok_ = 0, ol = 0;
+#pragma unroll
+      for (int u = 0; u < R; ++u) {
+        ok_ = u == k ? order[u] : ok_;
+        ol = u == l ? order[u] : ol;
+      }
+      double s0 = 0.0, q = 0.0;
+      for (int x = 0; x < N; ++x)
+        for (int y = 0; y < N; ++y) {
+          const double w = sV[x * N + ok_] * sV[y * N + ol];
+          s0 = fma(w, sM[x * N + y], s0);
+          q = fma(w, sD[x * N + y], q);
+        }
+      pr[P.S0 + L] = k == l ? s0 / n : 0.0;
+      pr[P.Q + L] = smooth_param * (q / (np_ - 1.0));
+    }
+    if (own && j < R) {
+      int oj = 0;
+#pragma unroll
+      for (int u = 0; u < R; ++u) oj = u == j ? order[u] : oj;
+      pr[P.C + i * R + j] = sV[i * N + oj];
+    }
+  }
+  if (status && L == 0) status[b] = n > 0.0 ? 0 : EKS_STATUS_SINGULAR;
+}
+
+// chunks per trajectory: enough lanes to fill the chip (~256k), chunks of
+// >= 64 frames, a multiple of kTile frames each
+void fit_chunks(long long B, long long T, int &nc, long long &lc) {
+  long long n = (262144 + B - 1) / (B > 0 ? B : 1);
+  const long long cap = T / 64 > 1 ? T / 64 : 1;
+  if (n > cap) n = cap;
+  if (n < 1) n = 1;
+  lc = (T + n - 1) / n;
+  lc = (lc + kTile - 1) / kTile * kTile;
+  nc = (int)((T + lc - 1) / lc);
+}
+
+constexpr int kMergeFan = 16;
+
+}  // namespace
+
+}  // namespace eks
+
+using namespace eks;
+
+extern "C" size_t eks_fit_workspace_bytes(int64_t B, int64_t T, int n) {
+  if (B <= 0 || T <= 0 || n < 1 || n > kMaxObs) return 0;
+  int nc;
+  long long lc;
+  fit_chunks(B, T, nc, lc);
+  const long long len = 2 + 4LL * n + (long long)n * (n + 1);
+  const long long nc2 = (nc + kMergeFan - 1) / kMergeFan;
+  return (size_t)(B * T + B + B * (nc + nc2) * len) * sizeof(double);
+}
+
+extern "C" int eks_fit(const void *obs, int obs_dtype, int64_t B, int64_t T, int E, int n, int r,
+                       int64_t sb, int64_t st, int64_t se, int64_t sj, int mode, int kind,
+                       double smooth_param, double quantile_keep, double *params,
+                       void *workspace, size_t workspace_bytes, int32_t *status, void *stream) {
+  clear_err();
+  if (!obs || !params || !workspace) return set_err(EKS_ERR_ARG, "eks_fit: NULL pointer");
+  if (B < 0 || T < 2 || E < 1 || n < 1) return set_err(EKS_ERR_ARG, "eks_fit: bad sizes");
+  if (B == 0) return EKS_OK;
+  if (E > kMaxMembers) return set_err(EKS_ERR_UNSUPPORTED, "eks_fit: E=%d > %d", E, kMaxMembers);
+  if (mode != EKS_MEDIAN && mode != EKS_MEAN)
+    return set_err(EKS_ERR_ARG, "%d averaging not supported", mode);
+  if (obs_dtype != EKS_F32 && obs_dtype != EKS_F64) return set_err(EKS_ERR_ARG, "bad dtype");
+  if (kind != EKS_FIT_SINGLEVIEW && kind != EKS_FIT_MULTICAM)
+    return set_err(EKS_ERR_ARG, "eks_fit: unknown model kind %d", kind);
+  if (kind == EKS_FIT_SINGLEVIEW && r != n)
+    return set_err(EKS_ERR_ARG, "eks_fit: single-view model needs r == n");
+  if (kind == EKS_FIT_MULTICAM && (r > n || r < 1))
+    return set_err(EKS_ERR_ARG, "eks_fit: PCA model needs 1 <= r <= n");
+  if (!(quantile_keep >= 0.0 && quantile_keep <= 100.0))
+    return set_err(EKS_ERR_ARG, "eks_fit: quantile_keep must be in [0, 100]");
+  if (workspace_bytes < eks_fit_workspace_bytes(B, T, n))
+    return set_err(EKS_ERR_ARG, "eks_fit: workspace too small (%zu < %zu)", workspace_bytes,
+                   eks_fit_workspace_bytes(B, T, n));
+  hipStream_t s = (hipStream_t)stream;
+  FitShape sh{B, T, 0, 0};
+  fit_chunks(B, T, sh.NC, sh.Lc);
+  const long long len = 2 + 4LL * n + (long long)n * (n + 1);
+  double *worst = (double *)workspace;
+  double *thr = worst + B * T;
+  double *partA = thr + B;
+  double *partB = partA + B * (long long)sh.NC * len;
+  // np.percentile 'linear': virtual index (T - 1) q / 100
+  const double vi = (double)(T - 1) * (quantile_keep / 100.0);
+  const long long lo = (long long)floor(vi);
+  const long long hi = lo + 1 < T ? lo + 1 : T - 1;
+  const double g = vi - (double)lo;
+  const int median = mode == EKS_MEDIAN ? 1 : 0;
+  const unsigned grid = grid_for(B * sh.NC, 256);
+  return dispatch_n(n, [&](auto Nc) {
+    constexpr int NN = decltype(Nc)::value;
+    auto by_type = [&](auto tag) -> int {
+      using Tp = decltype(tag);
+      auto by_e = [&](auto Ec) -> int {
+        constexpr int EE = decltype(Ec)::value;
+        prof_call_begin();
+        prof_mark(s, "k_fit_worst");
+        hipLaunchKernelGGL((k_fit_worst<EE, NN, Tp>), dim3(grid), dim3(256), 0, s,
+                           (const Tp *)obs, sh, sb, st, se, sj, E, median, worst);
+        int rc = check_launch("k_fit_worst");
+        if (rc) return rc;
+        prof_mark(s, "k_fit_select");
+        if (T >= 65536)
+          hipLaunchKernelGGL(k_fit_select<1024>, dim3((unsigned)B), dim3(1024), 0, s, worst, T,
+                             lo, hi, g, thr);
+        else
+          hipLaunchKernelGGL(k_fit_select<256>, dim3((unsigned)B), dim3(256), 0, s, worst, T, lo,
+                             hi, g, thr);
+        if ((rc = check_launch("k_fit_select"))) return rc;
+        prof_mark(s, "k_fit_accum");
+        hipLaunchKernelGGL((k_fit_accum<EE, NN, Tp>), dim3(grid), dim3(256), 0, s,
+                           (const Tp *)obs, sh, sb, st, se, sj, E, median, thr, partA);
+        if ((rc = check_launch("k_fit_accum"))) return rc;
+        // merge the chunk partials in order, kMergeFan at a time, ping-pong
+        double *src = partA, *dst = partB;
+        int nc = sh.NC;
+        while (nc > 1) {
+          const int nout = (nc + kMergeFan - 1) / kMergeFan;
+          const long long threads = B * (long long)nout * ChunkStats<NN>::kTri;
+          prof_mark(s, "k_fit_merge");
+          hipLaunchKernelGGL((k_fit_merge<NN>), dim3(grid_for(threads, 256)), dim3(256), 0, s, B,
+                             nc, kMergeFan, src, dst);
+          if ((rc = check_launch("k_fit_merge"))) return rc;
+          double *t = src;
+          src = dst;
+          dst = t;
+          nc = nout;
+        }
+        prof_mark(s, "k_fit_final");
+        rc = dispatch_r(r, [&](auto Rc) {
+          constexpr int RR = decltype(Rc)::value;
+          if constexpr (RR > NN) {
+            return set_err(EKS_ERR_ARG, "eks_fit: r > n");
+          } else {
+            hipLaunchKernelGGL((k_fit_final<RR, NN>), dim3((unsigned)B), dim3(64), 0, s, B, src,
+                               kind, smooth_param, params, status);
+            return check_launch("k_fit_final");
+          }
+        });
+        prof_call_end(s);
+        return rc;
+      };
+      switch (E) {
+        case 3: return by_e(ic<3>{});
+        case 4: return by_e(ic<4>{});
+        case 5: return by_e(ic<5>{});
+        default: return by_e(ic<0>{});
+      }
+    };
+    return obs_dtype == EKS_F32 ? by_type(float{}) : by_type(double{});
+  });
+}

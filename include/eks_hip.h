@@ -195,6 +195,25 @@ int eks_newton_filter(int64_t B, int64_t T, int n, int r, const double *y, const
                       int32_t *status, void *stream);
 
 /*
+ * eks_fit -- batched model fit (F2), replacing the per-keypoint host fit of
+ * eks/multiview_pca_smoother.py:684-731 (kind EKS_FIT_MULTICAM: PCA with r
+ * axes, r = 3 there) and the single-view model of SURVEY.md §8 A6 (kind
+ * EKS_FIT_SINGLEVIEW, r == n): good frames = max_j ensemble variance <=
+ * np.percentile(., quantile_keep); offset = mean of their ensemble
+ * predictions; S0 = diag(var of the good latents); Q = smooth_param *
+ * cov(diff(good latents)) (ddof 1); A = I; C = I or the principal axes.
+ * Writes params (B, eks_param_len(n, r)) for eks_smooth.  obs and strides
+ * as eks_smooth (T >= 2).  status (B) or NULL: EKS_STATUS_SINGULAR where no
+ * frame was kept (NaN threshold).  workspace: eks_fit_workspace_bytes.
+ */
+enum { EKS_FIT_SINGLEVIEW = 1, EKS_FIT_MULTICAM = 2 };
+size_t eks_fit_workspace_bytes(int64_t B, int64_t T, int n);
+int eks_fit(const void *obs, int obs_dtype, int64_t B, int64_t T, int E, int n, int r,
+            int64_t sb, int64_t st, int64_t se, int64_t sj, int mode, int kind,
+            double smooth_param, double quantile_keep, double *params, void *workspace,
+            size_t workspace_bytes, int32_t *status, void *stream);
+
+/*
  * Profiling aid (not part of the smoother's semantics).  After
  * eks_profile_begin(max_calls), each eks_smooth call on this thread records
  * a hipEvent on its stream before each of its kernels and after the last one

@@ -520,3 +520,92 @@ def test_opti_pupil_golden(torch):
     kps = ["pupil_top_r", "pupil_right_r", "pupil_bottom_r", "pupil_left_r"]
     res = eks_opti_smoother_pupil(dfs, kps, "ensemble-kalman_tracker", np.eye(3))
     assert np.abs(res["latents_df"].to_numpy() - g["golden_latents"]).max() < OUT_TOL
+
+
+# -------------------------------------------------------------------------
+# F2: batched model fit on the device (eks_fit) vs the host fit
+def _unpack(p, n, r):
+    o = 0
+    out = {}
+    for k, shp in (("m0", (r,)), ("S0", (r, r)), ("A", (r, r)), ("Q", (r, r)), ("C", (n, r)),
+                   ("offset", (n,))):
+        sz = int(np.prod(shp))
+        out[k] = p[o:o + sz].reshape(shp)
+        o += sz
+    return out
+
+
+@pytest.mark.parametrize("E,T,q,dtype", [(5, 3000, 25, "f32"), (3, 257, 10, "f64"),
+                                         (4, 2000, 50, "f32"), (5, 1001, 100, "f64"),
+                                         (7, 500, 0, "f64")])
+def test_fit_singleview_vs_host(torch, E, T, q, dtype):
+    from eks_amd import batch, fit, synthetic
+    from eks_amd.core import ensemble_array
+    rng = np.random.default_rng(E * T)
+    B = 6
+    st = np.stack([synthetic.singleview_obs(rng, E, T)[:, :, 0] for _ in range(B)])  # (B,E,T,2)
+    st = st.astype(np.float32 if dtype == "f32" else np.float64)
+    obs = torch.from_numpy(np.ascontiguousarray(st)).cuda().permute(0, 2, 1, 3)
+    params, status = batch.fit(obs, kind="singleview", n=2, r=2, smooth_param=0.01,
+                               quantile_keep=q)
+    params = params.cpu().numpy()
+    for b in range(B):
+        preds, ev = ensemble_array(st[b].astype(np.float64))
+        ref = fit.singleview_model(preds, ev, 0.01, q)
+        got = _unpack(params[b], 2, 2)
+        for k in ("m0", "S0", "A", "Q", "C", "offset"):
+            _close(got[k], ref[k], rtol=1e-9)
+
+
+@pytest.mark.parametrize("V,T", [(2, 2000), (4, 1500), (3, 700)])
+def test_fit_multicam_vs_host(torch, V, T):
+    from eks_amd import batch, fit, synthetic
+    from eks_amd.core import ensemble_array
+    rng = np.random.default_rng(V * T)
+    K, E = 3, 5
+    st = synthetic.multiview_obs(rng, V, E, T, K=K)  # (E, T, K, 2V) f32
+    stacks = np.ascontiguousarray(st.transpose(2, 0, 1, 3))  # (K, E, T, 2V)
+    obs = torch.from_numpy(stacks).cuda().permute(0, 2, 1, 3)
+    n = 2 * V
+    params, _ = batch.fit(obs, kind="multicam", n=n, r=3, smooth_param=0.01, quantile_keep=25)
+    params = params.cpu().numpy()
+    for k in range(K):
+        preds, ev = ensemble_array(stacks[k].astype(np.float64))
+        ref = fit.multicam_model(preds, ev, 0.01, 25)
+        got = _unpack(params[k], n, 3)
+        _close(got["offset"], ref["offset"], rtol=1e-9)
+        _close(got["A"], ref["A"])
+        # axes up to sign; S0 is sign-free, Q flips with the axis signs
+        sgn = np.sign(np.sum(got["C"] * ref["C"], axis=0))
+        _close(got["C"] * sgn, ref["C"], rtol=1e-7)
+        _close(got["S0"], ref["S0"], rtol=1e-8)
+        _close(got["Q"] * np.outer(sgn, sgn), ref["Q"], rtol=1e-7)
+
+
+def test_fit_then_smooth_matches_singleview_golden(torch):
+    """eks_fit + eks_smooth reproduce the committed single-view goldens."""
+    from eks_amd import batch
+    for path in sorted(glob.glob(os.path.join(GOLDEN, "singleview_*.npz"))):
+        g = np.load(path)
+        st = g["obs"]  # (E, T, 2)
+        obs = torch.from_numpy(np.ascontiguousarray(st, dtype=np.float64)).cuda()
+        obs = obs.permute(1, 0, 2).unsqueeze(0)
+        params, _ = batch.fit(obs, kind="singleview", n=2, r=2, smooth_param=float(g["s"]),
+                              quantile_keep=float(g["q"]))
+        out = batch.smooth(obs, params, n=2, r=2, check=True)["out"][0].cpu().numpy()
+        assert np.abs(out - g["out"]).max() < OUT_TOL, path
+
+
+def test_fit_then_smooth_matches_multicam_golden(torch):
+    from eks_amd import batch
+    for path in sorted(glob.glob(os.path.join(GOLDEN, "multicam_*.npz"))):
+        g = np.load(path)
+        stacks = g["stacks"]  # (V, E, T, 2)
+        st = np.concatenate(list(stacks), axis=2)  # (E, T, 2V)
+        n = st.shape[2]
+        obs = torch.from_numpy(np.ascontiguousarray(st, dtype=np.float64)).cuda()
+        obs = obs.permute(1, 0, 2).unsqueeze(0)
+        params, _ = batch.fit(obs, kind="multicam", n=n, r=3, smooth_param=float(g["s"]),
+                              quantile_keep=float(g["q"]))
+        out = batch.smooth(obs, params, n=n, r=3, check=True)["out"][0].cpu().numpy()
+        assert np.abs(out - g["golden"]).max() < OUT_TOL, path
