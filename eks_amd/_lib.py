@@ -50,6 +50,7 @@ SIGNATURES = {
     "eks_fit_workspace_bytes": (_sz, [_i64, _i64, _i32]),
     "eks_fit": (_i32, [_p, _i32, _i64, _i64, _i32, _i32, _i32, _i64, _i64, _i64, _i64, _i32, _i32,
                        C.c_double, C.c_double, _p, _p, _sz, _p, _p]),
+    "eks_interp1d": (_i32, [_p, _i64, _p, _i64, _i64, _i64, _p, _i64, _p, _i64, _i64, _p, _p]),
     "eks_profile_begin": (_i32, [_i32]),
     # include/eks_io.h (host-only)
     "eks_io_last_error": (C.c_char_p, []),

@@ -161,3 +161,33 @@ def singleview_model_batch(preds, ens_vars, smooth_param, quantile_keep):
     eye = torch.eye(n, dtype=preds.dtype, device=preds.device).expand(B, n, n)
     return dict(m0=torch.zeros(B, n, dtype=preds.dtype, device=preds.device), S0=S0,
                 A=eye.clone(), Q=Q, C=eye.clone(), offset=offset)
+
+
+def paw_async_models(cam_preds, cam_vars, smooth_param, quantile_keep):
+    """Model fit of the asynchronous paw smoother
+    (eks/multiview_pca_smoother.py:124-241).  cam_preds / cam_vars: (2, T, 4)
+    ensemble outputs of the left and the right (resampled, flipped) camera,
+    columns (paw 1 x, y, paw 2 x, y).  One PCA subspace is fitted on the good
+    frames of both paws stacked (2 rows per frame); each paw gets its own S0
+    and Q from its principal components.  Returns ([model paw 1, model paw
+    2], None); each model carries its centred observations 'y' and variances
+    'ev' (left view x, y, right view x, y)."""
+    lp, rp = cam_preds
+    lv, rv = cam_vars
+    worst = np.max(np.hstack([lv, rv]), 1)
+    good = np.flatnonzero(worst <= np.percentile(worst, quantile_keep))
+    stacked = np.empty((2 * len(good), 4))
+    stacked[0::2] = np.hstack([lp[good][:, :2], rp[good][:, :2]])
+    stacked[1::2] = np.hstack([lp[good][:, 2:4], rp[good][:, 2:4]])
+    means = stacked.mean(axis=0)
+    axes, centre = principal_axes(stacked - means, 3)
+    models = []
+    for k in range(2):
+        pred = np.hstack([lp[:, 2 * k:2 * k + 2], rp[:, 2 * k:2 * k + 2]])
+        var = np.hstack([lv[:, 2 * k:2 * k + 2], rv[:, 2 * k:2 * k + 2]])
+        y = pred - means
+        z_good = ((y - centre) @ axes.T)[good]
+        models.append(dict(m0=np.zeros(3), S0=np.diag(z_good.var(axis=0)), A=np.eye(3),
+                           Q=_step_cov(z_good, smooth_param), C=axes.T.copy(), offset=means,
+                           y=y, ev=var))
+    return models, None

@@ -206,13 +206,17 @@ def eks_opti_smoother_pupil(markers_list, keypoint_names, tracker_name, state_tr
 
 
 def ensemble_stacks(stacks, mode: str = "median"):
-    """(K, E, T, n) member array of K trajectories -> preds, vars (K, T, n)
-    CUDA float64, one eks_ensemble launch."""
+    """(K, E, T, n) member array (numpy or CUDA tensor) of K trajectories ->
+    (members on the device, preds, vars (K, T, n)) CUDA float64, one
+    eks_ensemble launch."""
     torch = _lib.require_gpu()
     if mode not in ("median", "mean"):
         raise ValueError(f"{mode} averaging not supported")
     K, E, T, n = stacks.shape
-    d = torch.from_numpy(np.ascontiguousarray(stacks, dtype=np.float64)).to("cuda")
+    if torch.is_tensor(stacks):
+        d = stacks.to(device="cuda", dtype=torch.float64).contiguous()
+    else:
+        d = torch.from_numpy(np.ascontiguousarray(stacks, dtype=np.float64)).to("cuda")
     preds = torch.empty((K, T, n), dtype=torch.float64, device="cuda")
     var = torch.empty_like(preds)
     lib = _lib.load()
@@ -261,3 +265,109 @@ __all__ = ["ensemble_kalman_smoother_multi_cam", "ensemble_kalman_smoother_pupil
            "ensemble_kalman_smoother_single_view", "pupil_smoothing_sweep",
            "eks_opti_smoother_multi_cam", "eks_opti_smoother_pupil", "multi_cam_batch",
            "ensemble_stacks", "TRACKER"]
+
+
+# --------------------------------------------------------------------------
+# F4: asynchronous two-camera paw smoother
+# --------------------------------------------------------------------------
+PAW_IMG_WIDTH = 128
+
+
+def interp1d_linear(x, y, xq):
+    """np.interp / interp1d(kind='linear') of every column of y (n, C) at xq,
+    on the GPU (eks_interp1d); bit-identical to numpy.  CUDA tensors in and
+    out (float64)."""
+    torch = _lib.require_gpu()
+    x = torch.as_tensor(x, dtype=torch.float64, device="cuda").contiguous()
+    xq = torch.as_tensor(xq, dtype=torch.float64, device="cuda").contiguous()
+    y = torch.as_tensor(y, dtype=torch.float64, device="cuda")
+    n, C = y.shape
+    out = torch.empty((len(xq), C), dtype=torch.float64, device="cuda")
+    status = torch.zeros(len(xq), dtype=torch.int32, device="cuda")
+    _lib.check(_lib.load().eks_interp1d(x.data_ptr(), n, y.data_ptr(), C, y.stride(0),
+                                        y.stride(1), xq.data_ptr(), len(xq), out.data_ptr(),
+                                        out.stride(0), out.stride(1), status.data_ptr(),
+                                        _lib.stream_ptr()), "eks_interp1d")
+    if bool((status != 0).any()):
+        raise ValueError("A value in x_new is outside the interpolation range.")
+    return out
+
+
+def _paw_async(markers_list_left_cam, markers_list_right_cam, timestamps_left_cam,
+               timestamps_right_cam, keypoint_names, smooth_param, quantile_keep_pca, opti):
+    torch = _lib.require_gpu()
+    tl = np.asarray(timestamps_left_cam, dtype=np.float64)
+    tr = np.asarray(timestamps_right_cam, dtype=np.float64)
+    # left-camera frames inside the right camera's time span, in the
+    # reference's loop order (:86-90): skip early frames, stop at the first late one
+    late = np.flatnonzero(tl > tr[-1])
+    stop = late[0] if len(late) else len(tl)
+    sel = np.flatnonzero(tl[:stop] >= tr[0])
+    cols = [0, 1, 3, 4]  # (x, y) of paw 1 and paw 2, likelihoods skipped
+    E = len(markers_list_left_cam)
+    left = np.stack([m.to_numpy()[sel][:, cols] for m in markers_list_left_cam])   # (E, T, 4)
+    right_raw = np.stack([m.to_numpy()[:, cols] for m in markers_list_right_cam])  # (E, Tr, 4)
+    T = len(sel)
+    # right camera resampled at the kept left timestamps, x flipped (:92-94)
+    rr = torch.from_numpy(np.ascontiguousarray(right_raw.transpose(1, 0, 2).reshape(len(tr), -1)))
+    right = interp1d_linear(tr, rr.cuda(), tl[sel]).reshape(T, E, 4).permute(1, 0, 2).contiguous()
+    right[:, :, 0] = PAW_IMG_WIDTH - right[:, :, 0]
+    right[:, :, 2] = PAW_IMG_WIDTH - right[:, :, 2]
+    cams = torch.stack([torch.from_numpy(left).cuda(), right])                    # (2, E, T, 4)
+    _, preds_d, ev_d = ensemble_stacks(cams)
+    preds, ev = preds_d.cpu().numpy(), ev_d.cpu().numpy()
+    models, paw_stacks = fit.paw_async_models(preds, ev, smooth_param, quantile_keep_pca)
+    st = lambda key: np.stack([m[key] for m in models])  # noqa: E731
+    n = 4
+    if opti:
+        y = np.stack([models[k]["y"] for k in range(2)])
+        v = np.stack([models[k]["ev"] for k in range(2)])
+        q, status = newton_filter_batch(y, v, st("m0"), st("S0"), st("A"), st("C"), st("Q"))
+        if bool((status != 0).any()):
+            raise np.linalg.LinAlgError("Singular matrix (kalman_newton_recursive)")
+        out = np.einsum("ktr,knr->ktn", q.cpu().numpy(), st("C")) + st("offset")[:, None, :]
+    else:
+        # per-paw member stacks (left view x, y | right view x, y): the fused
+        # smoother ensembles them again, bit-identically
+        obs = torch.stack([torch.cat([cams[0][:, :, 2 * k:2 * k + 2], cams[1][:, :, 2 * k:2 * k + 2]],
+                                     dim=2) for k in range(2)])                   # (2, E, T, 4)
+        params = batch.pack_params(st("m0"), st("S0"), st("A"), st("Q"), st("C"), st("offset"))
+        res = batch.smooth(obs.permute(0, 2, 1, 3), params, n=n, r=3,
+                           flags=_lib.EKS_MODEL_A_IDENTITY, check=True)
+        out = res["out"].cpu().numpy()
+    lp, rp = out[0], out[1]  # paw 1 / paw 2: (left x, y, right x, y)
+    nan = np.full(T, np.nan)
+    idx = make_dlc_pandas_index(keypoint_names)
+    df_left = pd.DataFrame(np.stack([lp[:, 0], lp[:, 1], nan, rp[:, 0], rp[:, 1], nan], 1),
+                           columns=idx)
+    # right view: paws swapped back and x flipped to the LP convention (:309-320)
+    df_right = pd.DataFrame(np.stack([PAW_IMG_WIDTH - rp[:, 2], rp[:, 3], nan,
+                                      PAW_IMG_WIDTH - lp[:, 2], lp[:, 3], nan], 1), columns=idx)
+    return {'left_df': df_left, 'right_df': df_right}
+
+
+def ensemble_kalman_smoother_paw_asynchronous(
+        markers_list_left_cam, markers_list_right_cam, timestamps_left_cam,
+        timestamps_right_cam, keypoint_names, smooth_param, quantile_keep_pca):
+    """Two asynchronous cameras, two paws (eks/multiview_pca_smoother.py:34-322):
+    the right camera is resampled at the left camera's timestamps (GPU linear
+    interpolation, eks_interp1d), one 3-D PCA subspace is fitted on both paws'
+    good frames, and both paws are smoothed in one batched eks_smooth call.
+    Returns {'left_df', 'right_df'} in the reference's layout."""
+    return _paw_async(markers_list_left_cam, markers_list_right_cam, timestamps_left_cam,
+                      timestamps_right_cam, keypoint_names, smooth_param, quantile_keep_pca,
+                      opti=False)
+
+
+def eks_opti_smoother_paw_asynchronous(
+        markers_list_left_cam, markers_list_right_cam, timestamps_left_cam,
+        timestamps_right_cam, keypoint_names, smooth_param, quantile_keep_pca):
+    """The same model with the Newton forward filter instead of the RTS
+    smoother (eks/multiview_pca_smoother.py:325-574)."""
+    return _paw_async(markers_list_left_cam, markers_list_right_cam, timestamps_left_cam,
+                      timestamps_right_cam, keypoint_names, smooth_param, quantile_keep_pca,
+                      opti=True)
+
+
+__all__ += ["ensemble_kalman_smoother_paw_asynchronous", "eks_opti_smoother_paw_asynchronous",
+            "interp1d_linear"]

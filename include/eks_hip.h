@@ -214,6 +214,20 @@ int eks_fit(const void *obs, int obs_dtype, int64_t B, int64_t T, int E, int n, 
             size_t workspace_bytes, int32_t *status, void *stream);
 
 /*
+ * eks_interp1d -- linear resampling for the asynchronous two-camera paw
+ * smoother (F4), replacing the scipy.interpolate.interp1d(kind='linear')
+ * calls of eks/multiview_pca_smoother.py:86-96 (which delegate to np.interp
+ * for 1-D float64 columns): out(q, c) = y interpolated at xq[q] for each of
+ * the ncol columns of y (element (k, c) at y[k*sy_row + c*sy_col]), sample
+ * times x (nx, ascending).  Bit-identical to np.interp.  status (nq) or NULL:
+ * EKS_STATUS_BAD_MODEL for queries outside [x[0], x[nx-1]] (interp1d raises
+ * there; the output is NaN).  Device pointers, f64.
+ */
+int eks_interp1d(const double *x, int64_t nx, const double *y, int64_t ncol, int64_t sy_row,
+                 int64_t sy_col, const double *xq, int64_t nq, double *out, int64_t so_row,
+                 int64_t so_col, int32_t *status, void *stream);
+
+/*
  * Profiling aid (not part of the smoother's semantics).  After
  * eks_profile_begin(max_calls), each eks_smooth call on this thread records
  * a hipEvent on its stream before each of its kernels and after the last one

@@ -395,3 +395,69 @@ def pupil_opti_smooth(stack, mode="median"):
     markers = q @ p["C"].T + p["means"]
     latents = np.stack([q[:, 0], q[:, 1] + p["mx"], q[:, 2] + p["my"]], axis=1)
     return markers, latents, p, ev
+
+
+# --------------------------------------------------------------------------
+# F4  asynchronous two-camera paw smoother
+#     (eks/multiview_pca_smoother.py:34-322 standard, :325-574 opti)
+# --------------------------------------------------------------------------
+PAW_IMG_WIDTH = 128
+
+
+def paw_async_select(tl, tr):
+    """Left-camera frames the reference keeps (:86-90): in order, skipping
+    ts < tr[0], stopping at the first ts > tr[-1]."""
+    keep = []
+    for i, ts in enumerate(tl):
+        if ts > tr[-1]:
+            break
+        if ts < tr[0]:
+            continue
+        keep.append(i)
+    return np.asarray(keep, dtype=np.int64)
+
+
+def paw_async_smooth(left_np, right_np, tl, tr, smooth_param, quantile_keep, opti=False):
+    """left_np / right_np: (E, T_cam, >= 5) member arrays (x, y, likelihood of
+    paw 1 then paw 2, as convert_lp_dlc orders them).  Returns (left (T, 4),
+    right (T, 4)) smoothed (x, y) pairs in the reference's output order:
+    left = (paw 1 x, y, paw 2 x, y) in the left view; right = (paw 2 x, y,
+    paw 1 x, y) in the right view, x flipped back (:300-320)."""
+    sel = paw_async_select(tl, tr)
+    cols = [0, 1, 3, 4]
+    E = left_np.shape[0]
+    Lc = np.stack([left_np[e][sel][:, cols] for e in range(E)])            # (E, T, 4)
+    Rc = np.stack([np.stack([np.interp(tl[sel], tr, right_np[e][:, j]) for j in cols], 1)
+                   for e in range(E)])
+    Rc[:, :, 0] = PAW_IMG_WIDTH - Rc[:, :, 0]
+    Rc[:, :, 2] = PAW_IMG_WIDTH - Rc[:, :, 2]
+    lp, lv = ensemble_array(Lc)
+    rp, rv = ensemble_array(Rc)
+    worst = np.max(np.hstack([lv, rv]), 1)
+    good = np.where(worst <= np.percentile(worst, quantile_keep))[0]
+    stacked = np.empty((2 * len(good), 4))
+    stacked[0::2] = np.hstack([lp[good][:, :2], rp[good][:, :2]])
+    stacked[1::2] = np.hstack([lp[good][:, 2:4], rp[good][:, 2:4]])
+    means = stacked.mean(axis=0)
+    comps, mean_ = pca_components(stacked - means, 3)
+    C = comps.T
+    paws = {"left": (np.hstack([lp[:, :2], rp[:, :2]]), np.hstack([lv[:, :2], rv[:, :2]])),
+            "right": (np.hstack([lp[:, 2:4], rp[:, 2:4]]), np.hstack([lv[:, 2:4], rv[:, 2:4]]))}
+    outs = {}
+    for paw, (pred, var) in paws.items():
+        y = pred - means
+        good_pcs = ((y - mean_) @ comps.T)[good]
+        S0 = np.diag(np.var(good_pcs, axis=0))
+        Q = smooth_param * np.cov((good_pcs[1:] - good_pcs[:-1]).T)
+        if opti:
+            q = kalman_newton_recursive(y, np.zeros(3), S0, np.eye(3), C, var, Q)
+        else:
+            R = np.eye(4)
+            mf, Vf, S = filtering_pass(y, np.zeros(3), S0, C, R, np.eye(3), Q, var)
+            q, _, _ = smooth_backward(y, mf, Vf, S, np.eye(3))
+        outs[paw] = q @ C.T + means
+    left = np.stack([outs["left"][:, 0], outs["left"][:, 1],
+                     outs["right"][:, 0], outs["right"][:, 1]], 1)
+    right = np.stack([PAW_IMG_WIDTH - outs["right"][:, 2], outs["right"][:, 3],
+                      PAW_IMG_WIDTH - outs["left"][:, 2], outs["left"][:, 3]], 1)
+    return left, right

@@ -93,3 +93,13 @@ def test_singleview_script_batches_videos(tmp_path):
             assert np.abs(a - b).max() < TOL
         lik = res.loc[:, (slice(None), slice(None), "likelihood")].to_numpy()
         assert (lik == 1.0).all()
+
+
+@pytest.mark.parametrize("version,prefix", [("standard", "kalman"), ("opti", "eks_opti")])
+def test_multiview_paw_script(tmp_path, version, prefix):
+    from eks_amd.scripts import multiview_paw_example
+    multiview_paw_example.main(["--csv-dir", os.path.join(CSV, "ibl-paw"), "--save-dir",
+                                str(tmp_path), "--eks_version", version])
+    for view in ("left", "right"):
+        name = f"{prefix}_smoothed_paw_traces.{view}.csv"
+        _cmp(tmp_path / name, os.path.join(EXP, name), [0, 1, 2])

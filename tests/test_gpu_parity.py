@@ -609,3 +609,39 @@ def test_fit_then_smooth_matches_multicam_golden(torch):
                               quantile_keep=float(g["q"]))
         out = batch.smooth(obs, params, n=n, r=3, check=True)["out"][0].cpu().numpy()
         assert np.abs(out - g["golden"]).max() < OUT_TOL, path
+
+
+# -------------------------------------------------------------------------
+# F4: asynchronous two-camera paw smoother
+def test_interp1d_bit_exact(torch):
+    from eks_amd.smoothers import interp1d_linear
+    rng = np.random.default_rng(7)
+    x = np.cumsum(rng.uniform(0.001, 0.05, size=500)) + 100.0
+    y = rng.normal(size=(500, 6)) * 50
+    y[17, 2] = np.nan
+    xq = np.sort(rng.uniform(x[0], x[-1], size=300))
+    xq[:3] = [x[0], x[10], x[-1]]  # exact sample times and both edges
+    got = interp1d_linear(x, y, xq).cpu().numpy()
+    ref = np.stack([np.interp(xq, x, y[:, c]) for c in range(6)], 1)
+    assert np.array_equal(got, ref, equal_nan=True), np.nanmax(np.abs(got - ref))
+    with pytest.raises(ValueError):
+        interp1d_linear(x, y, np.array([x[0] - 1.0]))
+
+
+@pytest.mark.parametrize("opti", [False, True])
+def test_paw_async_golden(torch, opti):
+    from eks_amd.multiview_pca_smoother import (ensemble_kalman_smoother_paw_asynchronous,
+                                                eks_opti_smoother_paw_asynchronous)
+    g = np.load(os.path.join(GOLDEN, "paw_async.npz"))
+    cols = ['paw_l_x', 'paw_l_y', 'paw_l_likelihood', 'paw_r_x', 'paw_r_y', 'paw_r_likelihood']
+    left = [pd.DataFrame(a, columns=cols) for a in g["left"]]
+    right = [pd.DataFrame(a, columns=cols) for a in g["right"]]
+    fn = eks_opti_smoother_paw_asynchronous if opti else ensemble_kalman_smoother_paw_asynchronous
+    d = fn(left, right, g["tl"], g["tr"], ["paw_l", "paw_r"], float(g["s"]), float(g["q"]))
+    k = "opti" if opti else "standard"
+    for view in ("left", "right"):
+        a = d[f"{view}_df"].to_numpy()
+        b = g[f"{k}_{view}"]
+        assert a.shape == b.shape
+        assert np.nanmax(np.abs(a - b)) < OUT_TOL
+        assert np.array_equal(np.isnan(a), np.isnan(b))

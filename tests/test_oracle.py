@@ -134,3 +134,26 @@ def test_newton_pupil_opti():
     _, latents, _, _ = O.pupil_opti_smooth(g["stack"])
     np.testing.assert_allclose(latents, g["latents"], rtol=0, atol=1e-9)
     np.testing.assert_allclose(latents, g["golden_latents"], rtol=0, atol=1e-9)
+
+
+@pytest.mark.parametrize("opti", [False, True])
+def test_paw_async(opti):
+    g = np.load(os.path.join(GOLDEN, "paw_async.npz"))
+    left, right = O.paw_async_smooth(g["left"], g["right"], g["tl"], g["tr"], float(g["s"]),
+                                     float(g["q"]), opti=opti)
+    k = "opti" if opti else "standard"
+    exp_l = g[f"{k}_left"].reshape(len(left), 2, 3)[:, :, :2].reshape(len(left), 4)
+    exp_r = g[f"{k}_right"].reshape(len(right), 2, 3)[:, :, :2].reshape(len(right), 4)
+    np.testing.assert_allclose(left, exp_l, rtol=0, atol=1e-8)
+    np.testing.assert_allclose(right, exp_r, rtol=0, atol=1e-8)
+    assert np.isnan(g[f"{k}_left"][:, 2]).all()
+
+
+def test_paw_select_and_interp():
+    g = np.load(os.path.join(GOLDEN, "paw_async.npz"))
+    from scipy.interpolate import interp1d
+    sel = O.paw_async_select(g["tl"], g["tr"])
+    assert len(sel) > 250
+    y = g["right"][0][:, 0]
+    a = interp1d(g["tr"], y)(g["tl"][sel])
+    assert np.array_equal(a, np.interp(g["tl"][sel], g["tr"], y))

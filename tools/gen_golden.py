@@ -404,8 +404,62 @@ def gen_cli(mv, ps, ut):
     print("  wrote expected pupil outputs")
 
 
+def gen_paw(mv, ut):
+    """ibl-paw (F4): the first 300 left-camera frames and the right-camera
+    frames spanning them, both eks versions of the asynchronous paw smoother
+    on them (eks/multiview_pca_smoother.py:34, :325), loaded as the
+    reference's scripts/multiview_paw_example.py:66-97 does (right-camera paws
+    swapped).  Timestamps read with numpy.load(allow_pickle=False)."""
+    src = os.path.join(REF, "data", "ibl-paw")
+    base = os.path.join(OUT, "csv", "ibl-paw")
+    os.makedirs(base, exist_ok=True)
+    stem = "3f859b5c-e73a-4044-b49e-34bb81e96715"
+    tl = np.load(os.path.join(src, f"{stem}.timestamps.left.npy"))
+    tr = np.load(os.path.join(src, f"{stem}.timestamps.right.npy"))
+    nl = 300
+    nr = int(np.searchsorted(tr, tl[nl - 1], side="right")) + 2
+    np.save(os.path.join(base, f"{stem}.timestamps.left.npy"), tl[:nl])
+    np.save(os.path.join(base, f"{stem}.timestamps.right.npy"), tr[:nr])
+    for f in sorted(glob.glob(os.path.join(src, "*.csv"))):
+        n = nl if ".left." in f else nr
+        lines = open(f).read().splitlines(True)
+        with open(os.path.join(base, os.path.basename(f)), "w") as fo:
+            fo.writelines(lines[:3 + n])
+    left, right = [], []
+    for f in sorted(glob.glob(os.path.join(base, "*.csv"))):
+        raw = pd.read_csv(f, header=[0, 1, 2], index_col=0)
+        kps = [c[1] for c in raw.columns[::3]]
+        fmt = ut.convert_lp_dlc(raw, kps, model_name=raw.columns[0][0])
+        if "left" in os.path.basename(f):
+            left.append(fmt)
+        else:
+            cols = {'paw_l_x': 'paw_r_x', 'paw_l_y': 'paw_r_y', 'paw_l_likelihood': 'paw_r_likelihood',
+                    'paw_r_x': 'paw_l_x', 'paw_r_y': 'paw_l_y', 'paw_r_likelihood': 'paw_l_likelihood'}
+            fmt = fmt.rename(columns=cols).loc[:, list(cols.keys())]
+            right.append(fmt)
+    exp = os.path.join(OUT, "csv", "expected")
+    os.makedirs(exp, exist_ok=True)
+    tl_, tr_ = tl[:nl], tr[:nr]
+    res = {}
+    for name, fn in (("standard", mv.ensemble_kalman_smoother_paw_asynchronous),
+                     ("opti", mv.eks_opti_smoother_paw_asynchronous)):
+        d = fn(left, right, tl_, tr_, kps, 1.0, 25)
+        prefix = "eks_opti" if name == "opti" else "kalman"
+        for view in ("left", "right"):
+            d[f"{view}_df"].to_csv(os.path.join(exp, f"{prefix}_smoothed_paw_traces.{view}.csv"))
+        res[name] = d
+    _save("paw_async",
+          left=np.stack([m.to_numpy() for m in left]), right=np.stack([m.to_numpy() for m in right]),
+          tl=tl_, tr=tr_, s=1.0, q=25.0,
+          **{f"{k}_{v}": res[k][f"{v}_df"].to_numpy() for k in res for v in ("left", "right")})
+    print("  wrote paw fixtures")
+
+
 def main():
     ek, mv, ps, ut = _import_reference()
+    if len(sys.argv) > 1 and sys.argv[1] == "paw":
+        gen_paw(mv, ut)
+        return
     if len(sys.argv) > 1 and sys.argv[1] == "cli":
         gen_cli(mv, ps, ut)
         return
@@ -420,6 +474,7 @@ def main():
     gen_pupil(ps, ut)
     gen_newton(mv, ps, ut)
     gen_cli(mv, ps, ut)
+    gen_paw(mv, ut)
 
 
 if __name__ == "__main__":
