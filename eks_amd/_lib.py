@@ -11,7 +11,8 @@ import os
 import re
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libeks_hip.so")
+# EKS_LIB overrides the library path (kernel tuning experiments only)
+LIB_PATH = os.environ.get("EKS_LIB") or os.path.join(HERE, "lib", "libeks_hip.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "eks_hip.h")
 HEADERS = [HEADER, os.path.join(os.path.dirname(HERE), "include", "eks_io.h")]
 

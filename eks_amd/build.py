@@ -29,7 +29,9 @@ OBJDIR = os.path.join(LIBDIR, "obj")
 LIBNAME = "libeks_hip.so"
 ARCH = os.environ.get("EKS_OFFLOAD_ARCH", "gfx950")
 HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
-CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall",
+# EKS_EXTRA_CFLAGS: tuning experiments only (e.g. "-DEKS_K3_D=2"), not used by default
+EXTRA = os.environ.get("EKS_EXTRA_CFLAGS", "").split()
+CFLAGS = [*EXTRA, "-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall",
           "-Wno-unused-function", "-Wno-unused-variable", "-Wno-unused-but-set-variable"]
 
 

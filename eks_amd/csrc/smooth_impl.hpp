@@ -82,6 +82,17 @@ inline long long wave_scan_chunks() {
   return v;
 }
 
+// waves per trajectory of the parallel chunk scans: enough that each thread
+// composes at most ~4 chunks before the in-wave scan
+inline int scan_waves(long long NC) {
+  static const int forced = [] {  // EKS_SCAN_WAVES: tuning / tests
+    const char *e = getenv("EKS_SCAN_WAVES");
+    return e ? atoi(e) : 0;
+  }();
+  if (forced == 1 || forced == 4 || forced == 8) return forced;
+  return NC > 512 ? 8 : (NC > 256 ? 4 : 1);
+}
+
 inline long long target_lanes() {
   static long long v = [] {
     const char *e = getenv("EKS_TARGET_LANES");
@@ -100,16 +111,34 @@ inline int state_len(int r) { return r + r * (r + 1) / 2; }
 
 inline long long round_up(long long x, long long m) { return (x + m - 1) / m * m; }
 
-// Chunk length L: short enough that B * NC lanes fill the GPU (L_fill), but
-// long enough that the chunk scans (which walk ~2 NC / 64 chunks per lane
-// sequentially) stay shorter than a chunk (L_scan = sqrt(2 T / 64)).
+inline bool uniform_lanes(long long B);
+
+// Chunk length L.
+// Many trajectories (whole blocks per chunk): short enough that B * NC lanes
+// fill the GPU (L_fill), long enough that the chunk scans stay short
+// (L_scan = sqrt(2 T / 64)).
+// Few trajectories (chunk-major lanes): the chip cannot be filled anyway, so
+// L balances the per-lane serial chunk work (~ L steps) against the serial
+// part of the block-parallel chunk scans (~ 2 NC / 512 element compositions):
+// L = sqrt(2 T rho / 512), rho = composition / step cost ratio, measured 2.6
+// for r <= 2 and 1.3 for r = 3 (configs 2, 3, 5: EKS_CHUNK_LEN sweeps).
 inline long long chunk_len(long long B, long long T, int r) {
-  (void)r;
   const long long ls = 8;  // a multiple of every checkpoint interval
-  const long long nc = std::max(1LL, (target_lanes() + B - 1) / B);
-  const long long l_fill = (T + nc - 1) / nc;
-  const long long l_scan = (long long)std::ceil(std::sqrt(2.0 * (double)T / 64.0));
-  long long L = std::max(kMinChunk, std::max(l_fill, l_scan));
+  static const long long forced = [] {  // EKS_CHUNK_LEN: tuning experiments only
+    const char *e = getenv("EKS_CHUNK_LEN");
+    return e ? atoll(e) : 0LL;
+  }();
+  if (forced > 0) return std::min(round_up(forced, ls), round_up(T, ls));
+  long long L;
+  if (uniform_lanes(B)) {
+    const long long nc = std::max(1LL, (target_lanes() + B - 1) / B);
+    const long long l_fill = (T + nc - 1) / nc;
+    const long long l_scan = (long long)std::ceil(std::sqrt(2.0 * (double)T / 64.0));
+    L = std::max(kMinChunk, std::max(l_fill, l_scan));
+  } else {
+    const double rho = r <= 2 ? 2.6 : 1.3;
+    L = std::max(kMinChunk, (long long)std::llround(std::sqrt(2.0 * (double)T * rho / 512.0)));
+  }
   L = round_up(L, ls);
   if (L >= T) L = round_up(T, ls);
   return L;
@@ -534,22 +563,24 @@ __global__ __launch_bounds__(64) void k_c2_fscan(SmoothArgs a, ChunkPlan p) {
   if (!ok) flag(a.status, b, EKS_STATUS_SCAN);
 }
 
-// K2, wave-parallel form: one wave per trajectory for many chunks.  Lane l
-// owns chunks [l q, (l+1) q): it composes their elements, the wave scans the
-// 64 aggregates (Hillis-Steele, log2 64 = 6 compositions), and each lane then
-// walks its chunks from its exclusive prefix.  Latency O(q + 6 + q) element
-// compositions instead of O(NC).
-template <int R, int N>
-__global__ __launch_bounds__(64) void k_c2_fscan_w(SmoothArgs a, ChunkPlan p) {
+// K2, parallel form: one block of W waves per trajectory for many chunks.
+// Thread l owns chunks [l q, (l+1) q): it composes their elements, each wave
+// scans its 64 aggregates (Hillis-Steele, log2 64 = 6 compositions), the
+// wave totals are combined through LDS (W - 1 compositions at most), and each
+// thread then walks its chunks from its exclusive prefix.  Latency
+// O(q + 6 + W + q) element compositions instead of O(NC).
+template <int R, int N, int W>
+__global__ __launch_bounds__(64 * W) void k_c2_fscan_w(SmoothArgs a, ChunkPlan p) {
+  __shared__ double tot[W][Elem<R>::len];
   const long long b = blockIdx.x;
-  const int l = threadIdx.x;
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
   const long long B = a.B, NC = p.NC;
   if (b >= B) return;
   constexpr int KS = R + Sym<R>::len;
   const double *elem = (const double *)(a.ws + p.elem_off);
   double *cst = (double *)(a.ws + p.cstart_off);
-  const long long q = (NC + 63) / 64;
-  const long long c0 = min(NC, (long long)l * q), c1 = min(NC, c0 + q);
+  const long long q = (NC + 64 * W - 1) / (64 * W);
+  const long long c0 = min(NC, (long long)tid * q), c1 = min(NC, c0 + q);
   bool ok = true;
   Elem<R> agg;
   agg.set_identity();
@@ -569,11 +600,33 @@ __global__ __launch_bounds__(64) void k_c2_fscan_w(SmoothArgs a, ChunkPlan p) {
       agg = t;
     }
   }
-  const Elem<R> ex = shfl_elem<R, true>(agg, 1);
+  Elem<R> ex = shfl_elem<R, true>(agg, 1);
+  if constexpr (W > 1) {
+    if (l == 0) ex.set_identity();
+    if (l == 63) agg.store(tot[w], 1);
+    __syncthreads();
+    if (w > 0) {  // prefix of the earlier waves' totals, in order
+      Elem<R> pre;
+      pre.load(tot[0], 1);
+      for (int v = 1; v < w; ++v) {
+        Elem<R> tv, t;
+        tv.load(tot[v], 1);
+        ok = compose_elem<R>(pre, tv, t) && ok;
+        pre = t;
+      }
+      if (l == 0) {
+        ex = pre;
+      } else {
+        Elem<R> t;
+        ok = compose_elem<R>(pre, ex, t) && ok;
+        ex = t;
+      }
+    }
+  }
   if (c0 < c1) {
     double m[R], P[R][R];
     long long c = c0;
-    if (l == 0) {
+    if (tid == 0) {
       using L = ParamLayout<R, N>;
       const double *pp = a.params + b * L::len;
       load_vec<R>(pp + L::m0, m);
@@ -644,22 +697,24 @@ struct Affine {
   }
 };
 
-// K4, wave-parallel form: chunk maps ms_start[c] = G_c ms_start[c+1] + g_c
-// composed right-to-left per lane, a suffix scan over lanes, then each lane
-// walks its chunks; NLL shares summed by a wave reduction.
-template <int R>
-__global__ __launch_bounds__(64) void k_c4_bscan_w(SmoothArgs a, ChunkPlan p) {
+// K4, parallel form: chunk maps ms_start[c] = G_c ms_start[c+1] + g_c
+// composed right-to-left per thread, a suffix scan over the lanes of each
+// wave, the wave totals combined through LDS, then each thread walks its
+// chunks; NLL shares summed by a block reduction (fixed order).
+template <int R, int W>
+__global__ __launch_bounds__(64 * W) void k_c4_bscan_w(SmoothArgs a, ChunkPlan p) {
+  __shared__ double tot[W][R * R + R];
+  __shared__ double nsum[W];
   const long long b = blockIdx.x;
-  const int l = threadIdx.x;
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
   const long long B = a.B, NC = p.NC;
   if (b >= B) return;
   const double *bw = (const double *)(a.ws + p.bwd_off);
   double *msend = (double *)(a.ws + p.msend_off);
-  const long long q = (NC + 63) / 64;
-  const long long c0 = min(NC, (long long)l * q), c1 = min(NC, c0 + q);
-  auto load_map = [&](long long c) {
+  const long long q = (NC + 64 * W - 1) / (64 * W);
+  const long long c0 = min(NC, (long long)tid * q), c1 = min(NC, c0 + q);
+  auto load_map = [&](const double *s) {
     Affine<R> f;
-    const double *s = bw + (b * NC + c) * (R * R + R);
 #pragma unroll
     for (int i = 0; i < R; ++i) {
       f.g[i] = s[R * R + i];
@@ -668,9 +723,10 @@ __global__ __launch_bounds__(64) void k_c4_bscan_w(SmoothArgs a, ChunkPlan p) {
     }
     return f;
   };
+  auto map_of = [&](long long c) { return load_map(bw + (b * NC + c) * (R * R + R)); };
   Affine<R> F;
   F.set_identity();
-  for (long long c = c1 - 1; c >= c0; --c) F = load_map(c).after(F);
+  for (long long c = c1 - 1; c >= c0; --c) F = map_of(c).after(F);
 #pragma unroll
   for (int k = 1; k < 64; k <<= 1) {
     const Affine<R> o = F.shfl_down(k);
@@ -678,6 +734,22 @@ __global__ __launch_bounds__(64) void k_c4_bscan_w(SmoothArgs a, ChunkPlan p) {
   }
   Affine<R> X = F.shfl_down(1);
   if (l == 63) X.set_identity();
+  if constexpr (W > 1) {
+    if (l == 0) {
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        tot[w][R * R + i] = F.g[i];
+#pragma unroll
+        for (int j = 0; j < R; ++j) tot[w][i * R + j] = F.G[i][j];
+      }
+    }
+    __syncthreads();
+    if (w + 1 < W) {  // suffix of the later waves' totals
+      Affine<R> S = load_map(tot[W - 1]);
+      for (int v = W - 2; v > w; --v) S = load_map(tot[v]).after(S);
+      X = X.after(S);
+    }
+  }
   double ms[R];
 #pragma unroll
   for (int i = 0; i < R; ++i) ms[i] = X.g[i];
@@ -686,7 +758,7 @@ __global__ __launch_bounds__(64) void k_c4_bscan_w(SmoothArgs a, ChunkPlan p) {
 #pragma unroll
       for (int i = 0; i < R; ++i) msend[(c * R + i) * B + b] = ms[i];
     }
-    const Affine<R> f = load_map(c);
+    const Affine<R> f = map_of(c);
     double nx[R];
 #pragma unroll
     for (int i = 0; i < R; ++i) {
@@ -704,7 +776,17 @@ __global__ __launch_bounds__(64) void k_c4_bscan_w(SmoothArgs a, ChunkPlan p) {
     for (long long c = c0; c < c1; ++c) s += np_[c * B + b];
 #pragma unroll
     for (int k = 32; k >= 1; k >>= 1) s += __shfl_xor(s, k, 64);
-    if (l == 0) a.nll[b] = s;
+    if constexpr (W > 1) {
+      if (l == 0) nsum[w] = s;
+      __syncthreads();
+      if (tid == 0) {
+        double t = nsum[0];
+        for (int v = 1; v < W; ++v) t += nsum[v];
+        a.nll[b] = t;
+      }
+    } else {
+      if (l == 0) a.nll[b] = s;
+    }
   }
 }
 
@@ -721,7 +803,9 @@ EKS_DEV void load_yev(const YT *ybuf, const double *evbuf, long long t, long lon
 
 template <int R, int N, typename YT, bool AI, bool CI, int LS, bool UNI>
 __global__ __launch_bounds__(kBlock) void k_c3_rerun(SmoothArgs a, ChunkPlan p) {
-  constexpr int D = LS < 4 ? LS : 4;  // y / ev prefetch distance (steps); divides LS
+  // y / ev prefetch distance (steps; divides LS): 2 keeps the (2, 2) kernel at
+  // 3 waves/SIMD (160 VGPRs), measured 3 % faster than 4 (174 VGPRs, 2 waves)
+  constexpr int D = (R <= 2 && N <= 2) ? 2 : (LS < 4 ? LS : 4);
   static_assert(LS % D == 0, "prefetch distance must divide the checkpoint interval");
   Lane<UNI> ln;
   const long long B = a.B, TT = a.T;
@@ -1019,11 +1103,19 @@ int launch_shape(const SmoothArgs &a, int algo, long long L) {
     // the chunk scans: one lane per trajectory while the chain is short, one
     // wave per trajectory (log-depth scan) when it is long
     const bool wave_scan = p.NC > wave_scan_chunks();
+    const int sw = scan_waves(p.NC);
     prof_mark(a.stream, "k_c2_fscan");
-    if (wave_scan)
-      hipLaunchKernelGGL((k_c2_fscan_w<R, N>), dim3((unsigned)a.B), dim3(64), 0, a.stream, a, p);
-    else
+    if (!wave_scan)
       hipLaunchKernelGGL((k_c2_fscan<R, N>), dim3(g64), dim3(64), 0, a.stream, a, p);
+    else if (sw == 8)
+      hipLaunchKernelGGL((k_c2_fscan_w<R, N, 8>), dim3((unsigned)a.B), dim3(512), 0, a.stream,
+                         a, p);
+    else if (sw == 4)
+      hipLaunchKernelGGL((k_c2_fscan_w<R, N, 4>), dim3((unsigned)a.B), dim3(256), 0, a.stream,
+                         a, p);
+    else
+      hipLaunchKernelGGL((k_c2_fscan_w<R, N, 1>), dim3((unsigned)a.B), dim3(64), 0, a.stream, a,
+                         p);
     if ((rc = check_launch("k_c2_fscan"))) return rc;
     prof_mark(a.stream, "k_c3_rerun");
     hipLaunchKernelGGL((k_c3_rerun<R, N, YT, AI, CI, LS, U>), dim3(gch), dim3(kBlock), 0,
@@ -1036,10 +1128,14 @@ int launch_shape(const SmoothArgs &a, int algo, long long L) {
       return check_launch("k_c4_nll");
     }
     prof_mark(a.stream, "k_c4_bscan");
-    if (wave_scan)
-      hipLaunchKernelGGL((k_c4_bscan_w<R>), dim3((unsigned)a.B), dim3(64), 0, a.stream, a, p);
-    else
+    if (!wave_scan)
       hipLaunchKernelGGL((k_c4_bscan<R>), dim3(g64), dim3(64), 0, a.stream, a, p);
+    else if (sw == 8)
+      hipLaunchKernelGGL((k_c4_bscan_w<R, 8>), dim3((unsigned)a.B), dim3(512), 0, a.stream, a, p);
+    else if (sw == 4)
+      hipLaunchKernelGGL((k_c4_bscan_w<R, 4>), dim3((unsigned)a.B), dim3(256), 0, a.stream, a, p);
+    else
+      hipLaunchKernelGGL((k_c4_bscan_w<R, 1>), dim3((unsigned)a.B), dim3(64), 0, a.stream, a, p);
     if ((rc = check_launch("k_c4_bscan"))) return rc;
     prof_mark(a.stream, "k_c5_final");
     hipLaunchKernelGGL((k_c5_final<R, N, YT, AI, CI, LS, U>), dim3(gch), dim3(kBlock), 0,
