@@ -63,3 +63,25 @@ def test_product_package_never_imports_oracle():
     for path in glob.glob(os.path.join(root, "eks_amd", "**", "*.py"), recursive=True):
         src = open(path).read()
         assert "oracle" not in src.replace("oracle/", ""), f"{path} references the oracle"
+
+
+def test_torch_ops_registered_with_fake_shapes():
+    """torch.ops.eks.* exist (SURVEY §8 B1) and propagate shapes without a GPU;
+    calling them on CPU tensors fails loudly (no CPU fallback)."""
+    import torch
+    from torch._subclasses.fake_tensor import FakeTensorMode
+    import eks_amd.ops as ops
+    for name in ops.OPS:
+        assert hasattr(torch.ops.eks, name)
+    with FakeTensorMode():
+        obs = torch.empty((3, 100, 5, 2), dtype=torch.float32)
+        params = torch.empty((3, 20), dtype=torch.float64)  # eks_param_len(2, 2)
+        out, st = torch.ops.eks.smooth(obs, params, 2, 2, "median", 0, 0)
+        assert out.shape == (3, 100, 2) and out.dtype == torch.float64 and st.shape == (3,)
+        p, s = torch.ops.eks.ensemble(obs, "median")
+        assert p.shape == (3, 100, 2)
+        prm, _ = torch.ops.eks.fit(obs, "singleview", 2, 2, 0.01, 25.0, "median")
+        assert prm.shape == (3, 20)
+        assert torch.ops.eks.nll(obs, params, 2, 2, "median", 0).shape == (3,)
+    with pytest.raises(RuntimeError, match="GPU only"):
+        torch.ops.eks.ensemble(torch.zeros((1, 4, 3, 2)), "median")

@@ -645,3 +645,20 @@ def test_paw_async_golden(torch, opti):
         assert a.shape == b.shape
         assert np.nanmax(np.abs(a - b)) < OUT_TOL
         assert np.array_equal(np.isnan(a), np.isnan(b))
+
+
+def test_torch_ops_match_batch_api(torch):
+    import eks_amd.ops  # noqa: F401
+    from eks_amd import batch, synthetic
+    rng = np.random.default_rng(11)
+    st = np.stack([synthetic.singleview_obs(rng, 5, 400)[:, :, 0] for _ in range(4)])
+    obs = torch.from_numpy(np.ascontiguousarray(st)).cuda().permute(0, 2, 1, 3)
+    params, _ = torch.ops.eks.fit(obs, "singleview", 2, 2, 0.01, 25.0, "median")
+    out, status = torch.ops.eks.smooth(obs, params, 2, 2, "median", 0, 0)
+    ref = batch.smooth(obs, params, n=2, r=2)["out"]
+    assert int(status.abs().sum()) == 0
+    assert torch.equal(out, ref.contiguous())
+    p, v = torch.ops.eks.ensemble(obs, "median")
+    assert p.shape == (4, 400, 2)
+    nll = torch.ops.eks.nll(obs, params, 2, 2, "median", 0)
+    assert torch.allclose(nll, batch.nll(obs, params, n=2, r=2), rtol=1e-12)
