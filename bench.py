@@ -196,7 +196,7 @@ def workload_singleview(torch, a, dev, rank, world, config):
             + f"{K} keypoints x {E} members x {T} frames, single-view EKS (ensemble median/var "
             f"-> forward KF -> RTS -> projection), float32 members, float64 recursions/outputs")
     return dict(step=step, fit_step=fit_step, status=status, units=B * T,
-                bytes_per_unit=E * 2 * 4 + 2 * 8, cpu=cpu, cpu_default=24 if config == 4 else 2, desc=desc,
+                bytes_per_unit=E * 2 * 4 + 2 * 8, cpu=cpu, cpu_default=64 if config == 4 else 4, desc=desc,
                 cfg=dict(videos=a.videos if config == 4 else 1, keypoints=K, members=E, frames=T,
                          trajectories_per_rank=B, smooth_param=a.smooth_param,
                          quantile_keep=a.quantile_keep),
@@ -242,7 +242,7 @@ def workload_multiview(torch, a, dev, rank, world):
     desc = (f"config 3: multiview PCA smoother, {V} cameras x {K} keypoints x {E} members x "
             f"{T} frames (r=3 latent, n=8), float32 members, float64 recursions/outputs")
     return dict(step=step, fit_step=fit_step, status=status, units=K * T,
-                bytes_per_unit=E * n * 4 + n * 8, cpu=cpu, cpu_default=2, desc=desc,
+                bytes_per_unit=E * n * 4 + n * 8, cpu=cpu, cpu_default=5, desc=desc,
                 cfg=dict(cameras=V, keypoints=K, members=E, frames=T,
                          smooth_param=a.smooth_param, quantile_keep=a.quantile_keep),
                 key=f"config3-multiview-k{K}-e{E}-t{T}-n{world}")
