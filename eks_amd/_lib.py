@@ -21,6 +21,7 @@ EKS_STATUS_SINGULAR, EKS_STATUS_BAD_MODEL, EKS_STATUS_SCAN = 1, 2, 4
 EKS_MODEL_A_IDENTITY, EKS_MODEL_C_IDENTITY = 1, 2
 EKS_FIT_SINGLEVIEW, EKS_FIT_MULTICAM = 1, 2
 EKS_F32, EKS_F64 = 0, 1
+EKS_YEV32, EKS_YEV64 = 2, 3
 EKS_MEDIAN, EKS_MEAN = 0, 1
 
 _p = C.c_void_p
@@ -50,7 +51,9 @@ SIGNATURES = {
                                  _p, _p, _p]),
     "eks_fit_workspace_bytes": (_sz, [_i64, _i64, _i32]),
     "eks_fit": (_i32, [_p, _i32, _i64, _i64, _i32, _i32, _i32, _i64, _i64, _i64, _i64, _i32, _i32,
-                       C.c_double, C.c_double, _p, _p, _sz, _p, _p]),
+                       C.c_double, C.c_double, _p, _p, _sz, _p, _p, _p]),
+    "eks_yev_dtype": (_i32, [_i32, _i32, _i32]),
+    "eks_yev_bytes": (_sz, [_i64, _i64, _i32, _i32, _i32, _i32]),
     "eks_interp1d": (_i32, [_p, _i64, _p, _i64, _i64, _i64, _p, _i64, _p, _i64, _i64, _p, _p]),
     "eks_profile_begin": (_i32, [_i32]),
     # include/eks_io.h (host-only)
@@ -65,8 +68,8 @@ def profile_begin(max_calls: int) -> None:
     check(load().eks_profile_begin(max_calls), "eks_profile_begin")
 
 
-def profile_end(max_kernels: int = 8):
-    """[(kernel name, total ms)] over the profiled eks_smooth calls."""
+def profile_end(max_kernels: int = 32):
+    """[(kernel name, total ms)] over the profiled calls (eks_smooth, eks_fit)."""
     ms = (C.c_double * max_kernels)()
     names = C.create_string_buffer(64 * max_kernels)
     k = load().eks_profile_end(ms, names, max_kernels, 64)

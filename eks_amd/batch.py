@@ -21,6 +21,19 @@ from . import _lib
 _WS = {}
 
 
+class Yev:
+    """Ensemble hand-off planes (y, ev) written by ``fit(..., keep_yev=True)``
+    and accepted by ``smooth`` in place of the member predictions (the
+    members are then read once for fit + smooth; include/eks_hip.h
+    eks_yev_bytes).  ``buf`` is a uint8 CUDA tensor; ``code`` the EKS_YEV32 /
+    EKS_YEV64 input code."""
+
+    def __init__(self, buf, B: int, T: int, E: int, n: int, code: int, mode: str):
+        self.buf, self.B, self.T, self.E, self.n, self.code, self.mode = buf, B, T, E, n, code, mode
+        self.shape = (B, T, E, n)
+        self.device = buf.device
+
+
 def param_len(n: int, r: int) -> int:
     return r + 3 * r * r + n * r + n
 
@@ -92,17 +105,25 @@ def smooth(obs, params, *, n: int, r: int, mode: str = "median", out=None, want_
     sequential algorithm if the time-parallel scan reported a breakdown.
     """
     torch = _lib.require_gpu()
-    if obs.dim() != 4:
-        raise ValueError("obs must be viewed as (B, T, E, n)")
-    B, T, E, nn = obs.shape
-    if nn != n:
-        raise ValueError(f"obs has {nn} coordinates, expected n={n}")
-    if obs.dtype == torch.float32:
-        dt = _lib.EKS_F32
-    elif obs.dtype == torch.float64:
-        dt = _lib.EKS_F64
+    if isinstance(obs, Yev):
+        B, T, E, nn = obs.shape
+        if nn != n:
+            raise ValueError(f"obs has {nn} coordinates, expected n={n}")
+        if mode != obs.mode:
+            raise ValueError("the hand-off planes were made in another averaging mode")
+        dt = obs.code
     else:
-        raise TypeError("obs must be float32 or float64")
+        if obs.dim() != 4:
+            raise ValueError("obs must be viewed as (B, T, E, n)")
+        B, T, E, nn = obs.shape
+        if nn != n:
+            raise ValueError(f"obs has {nn} coordinates, expected n={n}")
+        if obs.dtype == torch.float32:
+            dt = _lib.EKS_F32
+        elif obs.dtype == torch.float64:
+            dt = _lib.EKS_F64
+        else:
+            raise TypeError("obs must be float32 or float64")
     if mode not in ("median", "mean"):
         raise ValueError(f"{mode} averaging not supported")
     if params.shape != (B, param_len(n, r)) or params.dtype != torch.float64 \
@@ -120,10 +141,10 @@ def smooth(obs, params, *, n: int, r: int, mode: str = "median", out=None, want_
     lib = _lib.load()
     nbytes = lib.eks_smooth_workspace_bytes(B, T, n, r, E, algo)
     ws = workspace(nbytes, dev)
-    sb, st, se, sj = obs.stride()
+    sb, st, se, sj = (0, 0, 0, 0) if isinstance(obs, Yev) else obs.stride()
     ob, ot, oj = out.stride() if out is not None else (0, 0, 0)
     _lib.check(lib.eks_smooth(
-        obs.data_ptr(), dt, B, T, E, n, r, sb, st, se, sj,
+        obs.buf.data_ptr() if isinstance(obs, Yev) else obs.data_ptr(), dt, B, T, E, n, r, sb, st, se, sj,
         _lib.EKS_MEDIAN if mode == "median" else _lib.EKS_MEAN, params.data_ptr(),
         out.data_ptr() if out is not None else None, ob, ot, oj,
         ms.data_ptr() if ms is not None else None,
@@ -144,7 +165,7 @@ def smooth(obs, params, *, n: int, r: int, mode: str = "median", out=None, want_
 
 
 def fit(obs, *, kind: str, n: int, r: int, smooth_param: float, quantile_keep: float,
-        mode: str = "median", check: bool = True, params=None, status=None):
+        mode: str = "median", check: bool = True, params=None, status=None, keep_yev=False):
     """Batched model fit on the device (eks_fit, F2): (B, T, E, n) member view
     -> (B, eks_param_len(n, r)) float64 parameter rows for ``smooth``.
 
@@ -170,14 +191,26 @@ def fit(obs, *, kind: str, n: int, r: int, smooth_param: float, quantile_keep: f
         status = torch.empty((B,), dtype=torch.int32, device=obs.device)
     ws = workspace(lib.eks_fit_workspace_bytes(B, T, n), obs.device, slot="fit")
     sb, st, se, sj = obs.stride()
-    _lib.check(lib.eks_fit(obs.data_ptr(), dt, B, T, E, n, r, sb, st, se, sj,
-                           _lib.EKS_MEDIAN if mode == "median" else _lib.EKS_MEAN, k,
+    m = _lib.EKS_MEDIAN if mode == "median" else _lib.EKS_MEAN
+    yev = None
+    if keep_yev:
+        # a Yev object (reused when passed in) receives the ensemble planes
+        nbytes = lib.eks_yev_bytes(B, T, n, dt, E, m)
+        if isinstance(keep_yev, Yev) and keep_yev.buf.numel() >= nbytes:
+            yev = keep_yev
+        else:
+            yev = Yev(torch.empty(nbytes, dtype=torch.uint8, device=obs.device), B, T, E, n,
+                      lib.eks_yev_dtype(dt, E, m), mode)
+    _lib.check(lib.eks_fit(obs.data_ptr(), dt, B, T, E, n, r, sb, st, se, sj, m, k,
                            float(smooth_param), float(quantile_keep), params.data_ptr(),
-                           ws.data_ptr(), ws.numel(), status.data_ptr(), _lib.stream_ptr()),
+                           ws.data_ptr(), ws.numel(), status.data_ptr(),
+                           yev.buf.data_ptr() if yev is not None else None, _lib.stream_ptr()),
                "eks_fit")
     if check and bool((status != 0).any()):
         raise ValueError("eks_fit: no frame passed the variance threshold (NaN ensemble "
                          "variances?)")
+    if keep_yev:
+        return params, status, yev
     return params, status
 
 

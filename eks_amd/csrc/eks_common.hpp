@@ -65,6 +65,11 @@ struct ParamLayout {
 
 inline long long param_len(int n, int r) { return (long long)r + 3LL * r * r + (long long)n * r + n; }
 
+// byte offset of the ev planes in a y / ev hand-off buffer (eks_yev_bytes)
+__host__ __device__ inline size_t yev_ev_offset(long long B, long long T, int n, size_t ysize) {
+  return ((size_t)T * n * B * ysize + 255) / 256 * 256;
+}
+
 inline unsigned grid_for(long long work, int block) {
   long long g = (work + block - 1) / block;
   return (unsigned)(g < 1 ? 1 : g);

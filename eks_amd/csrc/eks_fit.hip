@@ -52,7 +52,7 @@ constexpr int kBins = 1 << kDigitBits;
 // like np.max)
 template <int E, int N, typename T>
 EKS_DEV void frame_ensemble(const T *p, long long se, long long sj, int Ert, bool median,
-                            double (&y)[N], double &v) {
+                            double (&y)[N], double (&ev)[N], double &v) {
   v = -1.0;
   bool nan = false;
 #pragma unroll
@@ -67,11 +67,39 @@ EKS_DEV void frame_ensemble(const T *p, long long se, long long sj, int Ert, boo
       ensemble_reduce_rt<T>(p + j * sj, se, Ert, median, avg, var);
     }
     y[j] = avg;
+    ev[j] = var;
     nan |= (var != var);
     v = var > v ? var : v;
   }
   if (nan) v = __builtin_nan("");
 }
+
+template <int E, int N, typename T>
+EKS_DEV void frame_ensemble(const T *p, long long se, long long sj, int Ert, bool median,
+                            double (&y)[N], double &v) {
+  double ev[N];
+  frame_ensemble<E, N, T>(p, se, sj, Ert, median, y, ev, v);
+}
+
+// the worst (largest) ensemble variance of a frame from its ev values
+template <int N>
+EKS_DEV double worst_of(const double (&ev)[N]) {
+  double v = -1.0;
+  bool nan = false;
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    nan |= (ev[j] != ev[j]);
+    v = ev[j] > v ? ev[j] : v;
+  }
+  return nan ? __builtin_nan("") : v;
+}
+
+// y / ev hand-off planes (eks_smooth EKS_YEV32 / EKS_YEV64 input):
+// time-major [t*N + j][b], y of type YT then ev (f64) 256-byte aligned
+struct YevOut {
+  void *y = nullptr;
+  double *ev = nullptr;
+};
 
 struct FitShape {
   long long B, T;
@@ -81,11 +109,11 @@ struct FitShape {
 
 constexpr int kTile = 16;  // frames per register tile: one 128-byte row segment per lane
 
-template <int E, int N, typename T>
+template <int E, int N, typename T, typename YT>
 __global__ __launch_bounds__(256) void k_fit_worst(const T *__restrict__ obs, FitShape sh,
                                                    long long sb, long long st, long long se,
                                                    long long sj, int Ert, int median,
-                                                   double *__restrict__ worst) {
+                                                   double *__restrict__ worst, YevOut yo) {
   // each lane computes kTile consecutive frames of its (trajectory, chunk)
   // into LDS; the block then writes the trajectory-major rows as whole
   // 128-byte segments (16 lanes per segment) instead of one 8-byte store
@@ -107,18 +135,30 @@ __global__ __launch_bounds__(256) void k_fit_worst(const T *__restrict__ obs, Fi
     if (active && t + kTile <= t1) {
 #pragma unroll
       for (int k = 0; k < kTile; ++k) {
-        double y[N];
-        frame_ensemble<E, N, T>(pb + (t + k) * st, se, sj, Ert, median != 0, y,
+        double y[N], ev[N];
+        frame_ensemble<E, N, T>(pb + (t + k) * st, se, sj, Ert, median != 0, y, ev,
                                 tile[threadIdx.x][k]);
+        if (yo.y)
+#pragma unroll
+          for (int j = 0; j < N; ++j) {
+            ((YT *)yo.y)[((t + k) * N + j) * sh.B + b] = (YT)y[j];
+            yo.ev[((t + k) * N + j) * sh.B + b] = ev[j];
+          }
       }
       base[threadIdx.x] = b * sh.T + t;
     } else {
       base[threadIdx.x] = -1;
       if (active)
         for (long long u = t; u < t1; ++u) {  // ragged end of the last chunk
-          double y[N], v;
-          frame_ensemble<E, N, T>(pb + u * st, se, sj, Ert, median != 0, y, v);
+          double y[N], ev[N], v;
+          frame_ensemble<E, N, T>(pb + u * st, se, sj, Ert, median != 0, y, ev, v);
           worst[b * sh.T + u] = v;
+          if (yo.y)
+#pragma unroll
+            for (int j = 0; j < N; ++j) {
+              ((YT *)yo.y)[(u * N + j) * sh.B + b] = (YT)y[j];
+              yo.ev[(u * N + j) * sh.B + b] = ev[j];
+            }
         }
     }
     __syncthreads();
@@ -371,12 +411,12 @@ EKS_DEV constexpr int tri(int i, int j) {  // i <= j
   return i * N - i * (i - 1) / 2 + (j - i);
 }
 
-template <int E, int N, typename T>
+template <int E, int N, typename T, typename YT, bool FROM_YEV>
 __global__ __launch_bounds__(256) void k_fit_accum(const T *__restrict__ obs, FitShape sh,
                                                    long long sb, long long st, long long se,
                                                    long long sj, int Ert, int median,
                                                    const double *__restrict__ thr,
-                                                   double *__restrict__ part) {
+                                                   double *__restrict__ part, YevOut yi) {
   using CS = ChunkStats<N>;
   const long long lane = blockIdx.x * (long long)blockDim.x + threadIdx.x;
   if (lane >= sh.B * sh.NC) return;
@@ -393,7 +433,17 @@ __global__ __launch_bounds__(256) void k_fit_accum(const T *__restrict__ obs, Fi
   for (int i = 0; i < CS::kTri; ++i) S2[i] = D2[i] = 0.0;
   for (long long t = t0; t < t1; ++t) {
     double y[N], v;
-    frame_ensemble<E, N, T>(pb + t * st, se, sj, Ert, median != 0, y, v);
+    if constexpr (FROM_YEV) {  // the ensemble of this frame is already in the planes
+      double ev[N];
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        y[j] = (double)((const YT *)yi.y)[(t * N + j) * sh.B + b];
+        ev[j] = yi.ev[(t * N + j) * sh.B + b];
+      }
+      v = worst_of<N>(ev);
+    } else {
+      frame_ensemble<E, N, T>(pb + t * st, se, sj, Ert, median != 0, y, v);
+    }
     if (!(v <= th)) continue;
     if (cnt == 0.0) {
 #pragma unroll
@@ -670,10 +720,27 @@ extern "C" size_t eks_fit_workspace_bytes(int64_t B, int64_t T, int n) {
   return (size_t)(B * T + B + B * (nc + nc2) * len) * sizeof(double);
 }
 
+// y of the hand-off planes is float32 exactly when it is a member value:
+// float32 members, median mode, odd E the smoother specialises (3, 5)
+static bool yev_float(int obs_dtype, int E, int mode) {
+  return obs_dtype == EKS_F32 && mode == EKS_MEDIAN && (E == 3 || E == 5);
+}
+
+extern "C" int eks_yev_dtype(int obs_dtype, int E, int mode) {
+  return yev_float(obs_dtype, E, mode) ? EKS_YEV32 : EKS_YEV64;
+}
+
+extern "C" size_t eks_yev_bytes(int64_t B, int64_t T, int n, int obs_dtype, int E, int mode) {
+  if (B <= 0 || T <= 0 || n < 1) return 0;
+  const size_t ys = yev_float(obs_dtype, E, mode) ? 4 : 8;
+  return yev_ev_offset(B, T, n, ys) + (size_t)B * T * n * 8;
+}
+
 extern "C" int eks_fit(const void *obs, int obs_dtype, int64_t B, int64_t T, int E, int n, int r,
                        int64_t sb, int64_t st, int64_t se, int64_t sj, int mode, int kind,
                        double smooth_param, double quantile_keep, double *params,
-                       void *workspace, size_t workspace_bytes, int32_t *status, void *stream) {
+                       void *workspace, size_t workspace_bytes, int32_t *status, void *yev,
+                       void *stream) {
   clear_err();
   if (!obs || !params || !workspace) return set_err(EKS_ERR_ARG, "eks_fit: NULL pointer");
   if (B < 0 || T < 2 || E < 1 || n < 1) return set_err(EKS_ERR_ARG, "eks_fit: bad sizes");
@@ -708,16 +775,23 @@ extern "C" int eks_fit(const void *obs, int obs_dtype, int64_t B, int64_t T, int
   const double g = vi - (double)lo;
   const int median = mode == EKS_MEDIAN ? 1 : 0;
   const unsigned grid = grid_for(B * sh.NC, 256);
+  const bool y32 = yev_float(obs_dtype, E, mode);
+  YevOut yo;
+  if (yev) {
+    yo.y = yev;
+    yo.ev = (double *)((char *)yev + yev_ev_offset(B, T, n, y32 ? 4 : 8));
+  }
   return dispatch_n(n, [&](auto Nc) {
     constexpr int NN = decltype(Nc)::value;
-    auto by_type = [&](auto tag) -> int {
+    auto by_type = [&](auto tag, auto ytag) -> int {
       using Tp = decltype(tag);
+      using YT = decltype(ytag);
       auto by_e = [&](auto Ec) -> int {
         constexpr int EE = decltype(Ec)::value;
         prof_call_begin();
         prof_mark(s, "k_fit_worst");
-        hipLaunchKernelGGL((k_fit_worst<EE, NN, Tp>), dim3(grid), dim3(256), 0, s,
-                           (const Tp *)obs, sh, sb, st, se, sj, E, median, worst);
+        hipLaunchKernelGGL((k_fit_worst<EE, NN, Tp, YT>), dim3(grid), dim3(256), 0, s,
+                           (const Tp *)obs, sh, sb, st, se, sj, E, median, worst, yo);
         int rc = check_launch("k_fit_worst");
         if (rc) return rc;
         prof_mark(s, "k_fit_select");
@@ -729,8 +803,14 @@ extern "C" int eks_fit(const void *obs, int obs_dtype, int64_t B, int64_t T, int
                              hi, g, thr);
         if ((rc = check_launch("k_fit_select"))) return rc;
         prof_mark(s, "k_fit_accum");
-        hipLaunchKernelGGL((k_fit_accum<EE, NN, Tp>), dim3(grid), dim3(256), 0, s,
-                           (const Tp *)obs, sh, sb, st, se, sj, E, median, thr, partA);
+        // with the hand-off planes written, the second pass reads them (24 B
+        // per frame for n = 2) instead of the members (40 B) and skips the sort
+        if (yev)
+          hipLaunchKernelGGL((k_fit_accum<EE, NN, Tp, YT, true>), dim3(grid), dim3(256), 0, s,
+                             (const Tp *)obs, sh, sb, st, se, sj, E, median, thr, partA, yo);
+        else
+          hipLaunchKernelGGL((k_fit_accum<EE, NN, Tp, YT, false>), dim3(grid), dim3(256), 0, s,
+                             (const Tp *)obs, sh, sb, st, se, sj, E, median, thr, partA, yo);
         if ((rc = check_launch("k_fit_accum"))) return rc;
         // merge the chunk partials in order, kMergeFan at a time, ping-pong
         double *src = partA, *dst = partB;
@@ -768,6 +848,7 @@ extern "C" int eks_fit(const void *obs, int obs_dtype, int64_t B, int64_t T, int
         default: return by_e(ic<0>{});
       }
     };
-    return obs_dtype == EKS_F32 ? by_type(float{}) : by_type(double{});
+    if (y32) return by_type(float{}, float{});
+    return obs_dtype == EKS_F32 ? by_type(float{}, double{}) : by_type(double{}, double{});
   });
 }

@@ -51,7 +51,9 @@ int eks_smooth(const void *obs, int obs_dtype, int64_t B, int64_t T, int E, int 
   if (E > kMaxMembers) return set_err(EKS_ERR_UNSUPPORTED, "eks_smooth: E=%d > %d", E, kMaxMembers);
   if (mode != EKS_MEDIAN && mode != EKS_MEAN)
     return set_err(EKS_ERR_ARG, "%d averaging not supported", mode);
-  if (obs_dtype != EKS_F32 && obs_dtype != EKS_F64) return set_err(EKS_ERR_ARG, "bad dtype");
+  if (obs_dtype != EKS_F32 && obs_dtype != EKS_F64 && obs_dtype != EKS_YEV32 &&
+      obs_dtype != EKS_YEV64)
+    return set_err(EKS_ERR_ARG, "bad dtype");
   if (algo < 0 || algo > 2) return set_err(EKS_ERR_ARG, "eks_smooth: algo %d unknown", algo);
   if (!shape_supported(r, n))
     return set_err(EKS_ERR_UNSUPPORTED,

@@ -154,6 +154,9 @@ struct ChunkPlan {
   EKS_DEV unsigned ylane(unsigned b) const { return yB == 1 ? 0u : b; }
   size_t y_off = 0, ev_off = 0, elem_off = 0, cstart_off = 0, bwd_off = 0, nllp_off = 0,
          msend_off = 0, ckpt_off = 0, total = 0;
+  // where K3 / K5 read y / ev: the workspace planes K1 wrote, or (EKS_YEV
+  // input) the caller's planes
+  const char *ysrc = nullptr, *evsrc = nullptr;
 };
 
 inline size_t align256(size_t x) { return (x + 255) / 256 * 256; }
@@ -264,6 +267,27 @@ EKS_DEV void flag(int32_t *status, long long b, int bits) {
   if (bits) atomicOr(status + b, bits);
 }
 
+// Input tag: instead of member predictions the caller hands over the
+// ensemble output itself (y / ev planes written by eks_fit, EKS_YEV32/64),
+// time-major [t*N + j][b]: y of type YT, then ev (f64) at yev_ev_offset.
+template <typename YT>
+struct YevIn {
+  using y_type = YT;
+};
+template <typename T>
+struct is_yev : std::false_type {};
+template <typename YT>
+struct is_yev<YevIn<YT>> : std::true_type {};
+template <typename T>
+struct yev_y {
+  using type = T;
+};
+template <typename YT>
+struct yev_y<YevIn<YT>> {
+  using type = YT;
+};
+
+
 // ===========================================================================
 // algo 1: one lane per trajectory, sequential in time
 // ===========================================================================
@@ -279,7 +303,6 @@ __global__ __launch_bounds__(64) void k_smooth_seq(SmoothArgs a) {
   md.load(a.params + b * ParamLayout<R, N>::len, true);
   if (!md.template valid<AI, CI>()) flag(a.status, b, EKS_STATUS_BAD_MODEL);
   double *ws = (double *)a.ws;
-  const T *ob = (const T *)a.obs + b * a.sb;
   double *outb = a.out + b * a.ob;
   bool ok = true;
   NllAcc acc;
@@ -290,25 +313,45 @@ __global__ __launch_bounds__(64) void k_smooth_seq(SmoothArgs a) {
 #pragma unroll
     for (int j = 0; j < R; ++j) P[i][j] = md.S0[i][j];
   }
-  T cur[EE][N], nxt[EE][N];
-  if constexpr (E > 0) load_step<E, N, T>(ob, a.se, a.sj, cur);
-  for (long long t = 0; t < TT; ++t) {
-    const T *pt = ob + t * a.st;
-    if constexpr (E > 0) {
-      if (t + 1 < TT) load_step<E, N, T>(pt + a.st, a.se, a.sj, nxt);
-    }
-    double y[N], rv[N];
-    reduce_step<E, N, T>(cur, pt, a.se, a.sj, a.E, median, y, rv);
+  auto step = [&](long long t, double (&y)[N], const double (&rv)[N]) {
 #pragma unroll
     for (int j = 0; j < N; ++j) y[j] -= md.off[j];
     if (t > 0) kf_predict<R, AI>(m, P, md.A, md.Q);
     kf_update<R, N, CI>(m, P, md.C, y, rv, acc, ok);
     store_state<R>(ws + t * K * B + b, B, m, P);
-    if constexpr (E > 0) {
+  };
+  if constexpr (is_yev<T>::value) {  // ensemble handed over as y / ev planes
+    using YT = typename yev_y<T>::type;
+    const YT *yb = (const YT *)a.obs;
+    const double *eb =
+        (const double *)((const char *)a.obs + yev_ev_offset(B, TT, N, sizeof(YT)));
+    for (long long t = 0; t < TT; ++t) {
+      double y[N], rv[N];
 #pragma unroll
-      for (int e = 0; e < E; ++e)
+      for (int j = 0; j < N; ++j) {
+        y[j] = (double)yb[(t * N + j) * B + b];
+        rv[j] = eb[(t * N + j) * B + b];
+      }
+      step(t, y, rv);
+    }
+  } else {
+    const T *ob = (const T *)a.obs + b * a.sb;
+    T cur[EE][N], nxt[EE][N];
+    if constexpr (E > 0) load_step<E, N, T>(ob, a.se, a.sj, cur);
+    for (long long t = 0; t < TT; ++t) {
+      const T *pt = ob + t * a.st;
+      if constexpr (E > 0) {
+        if (t + 1 < TT) load_step<E, N, T>(pt + a.st, a.se, a.sj, nxt);
+      }
+      double y[N], rv[N];
+      reduce_step<E, N, T>(cur, pt, a.se, a.sj, a.E, median, y, rv);
+      step(t, y, rv);
+      if constexpr (E > 0) {
 #pragma unroll
-        for (int j = 0; j < N; ++j) cur[e][j] = nxt[e][j];
+        for (int e = 0; e < E; ++e)
+#pragma unroll
+          for (int j = 0; j < N; ++j) cur[e][j] = nxt[e][j];
+      }
     }
   }
   if (a.nll) a.nll[b] = acc.value((double)TT * N);
@@ -429,8 +472,44 @@ EKS_DEV void load_state_pl(const double *base, long long plane0, long long B, un
 template <int E, int N, typename T, typename YT, int D, typename Absorb>
 EKS_DEV void c1_stream(const SmoothArgs &a, const ChunkPlan &p, long long s, long long e,
                        unsigned b, const double (&off)[N], Absorb &&absorb) {
-  constexpr int EE = E > 0 ? E : 1;
   const long long B = a.B;
+  if constexpr (is_yev<T>::value) {
+    // the ensemble is already in the caller's planes: stream y / ev
+    constexpr int DY = 2;
+    YT yr[DY][N];
+    double er[DY][N];
+#pragma unroll
+    for (int q = 0; q < DY; ++q)
+      if (s + q < e)
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+          yr[q][j] = pl((const YT *)p.ysrc, (s + q) * N + j, B, b);
+          er[q][j] = pl((const double *)p.evsrc, (s + q) * N + j, B, b);
+        }
+    for (long long t0 = s; t0 < e; t0 += DY) {
+#pragma unroll
+      for (int q = 0; q < DY; ++q) {
+        const long long t = t0 + q;
+        if (t < e) {
+          double y[N], rv[N];
+#pragma unroll
+          for (int j = 0; j < N; ++j) {
+            y[j] = (double)yr[q][j] - off[j];
+            rv[j] = er[q][j];
+          }
+          if (t + DY < e)
+#pragma unroll
+            for (int j = 0; j < N; ++j) {
+              yr[q][j] = pl((const YT *)p.ysrc, (t + DY) * N + j, B, b);
+              er[q][j] = pl((const double *)p.evsrc, (t + DY) * N + j, B, b);
+            }
+          absorb(t, y, rv);
+        }
+      }
+    }
+    return;
+  } else {
+  constexpr int EE = E > 0 ? E : 1;
   const bool median = a.median != 0;
   YT *ybuf = (YT *)(a.ws + p.y_off);
   double *evbuf = (double *)(a.ws + p.ev_off);
@@ -468,6 +547,7 @@ EKS_DEV void c1_stream(const SmoothArgs &a, const ChunkPlan &p, long long s, lon
         absorb(t, y, rv);
       }
     }
+  }
   }
 }
 
@@ -815,8 +895,8 @@ __global__ __launch_bounds__(kBlock) void k_c3_rerun(SmoothArgs a, ChunkPlan p) 
   constexpr int KS = R + Sym<R>::len;
   Model<R, N> md;
   md.load(a.params + (long long)b * ParamLayout<R, N>::len, false);
-  const YT *ybuf = (const YT *)(a.ws + p.y_off);
-  const double *evbuf = (const double *)(a.ws + p.ev_off);
+  const YT *ybuf = (const YT *)p.ysrc;
+  const double *evbuf = (const double *)p.evsrc;
   double *ckpt = (double *)(a.ws + p.ckpt_off);
   double m[R], P[R][R];
   load_state_pl<R>((const double *)(a.ws + p.cstart_off), c * KS, B, b, m, P);
@@ -973,8 +1053,8 @@ __global__ __launch_bounds__(kBlock) void k_c5_final(SmoothArgs a, ChunkPlan p) 
   constexpr int KS = R + Sym<R>::len;
   Model<R, N> md;
   md.load(a.params + (long long)b * ParamLayout<R, N>::len, false);
-  const YT *ybuf = (const YT *)(a.ws + p.y_off);
-  const double *evbuf = (const double *)(a.ws + p.ev_off);
+  const YT *ybuf = (const YT *)p.ysrc;
+  const double *evbuf = (const double *)p.evsrc;
   const double *ckpt = (const double *)(a.ws + p.ckpt_off);
   double ms[R];
   if (c + 1 < p.NC) {
@@ -1062,7 +1142,20 @@ int dispatch_members_c(int E, F &&f) {
 template <int R, int N, bool AI, bool CI>
 int launch_shape(const SmoothArgs &a, int algo, long long L) {
   const bool f32 = a.dtype == EKS_F32;
+  const bool yev = a.dtype == EKS_YEV32 || a.dtype == EKS_YEV64;
   if (algo == 1) {
+    if (yev) {
+      auto go_yev = [&](auto ytag) -> int {
+        using YT = decltype(ytag);
+        prof_call_begin();
+        prof_mark(a.stream, "k_smooth_seq");
+        hipLaunchKernelGGL((k_smooth_seq<R, N, 0, YevIn<YT>, AI, CI>), dim3(grid_for(a.B, 64)),
+                           dim3(64), 0, a.stream, a);
+        prof_call_end(a.stream);
+        return check_launch("k_smooth_seq");
+      };
+      return a.dtype == EKS_YEV32 ? go_yev(float{}) : go_yev(double{});
+    }
     auto go = [&](auto tag) -> int {
       using Tp = decltype(tag);
       return dispatch_members_c(a.E, [&](auto Ec) {
@@ -1079,26 +1172,38 @@ int launch_shape(const SmoothArgs &a, int algo, long long L) {
   }
   ChunkPlan p = make_plan(a.B, a.T, R, N, L);
   p.smooth = a.out != nullptr;
-  p.yB = (a.sb == 0 && a.B > 1) ? 1 : a.B;
+  p.yB = (!yev && a.sb == 0 && a.B > 1) ? 1 : a.B;
   const bool uni = uniform_lanes(a.B);
   const unsigned gch = uni ? (unsigned)(p.NC * blocks_per_chunk(a.B))
                            : grid_for(p.NC * a.B, kBlock);
   const unsigned g64 = grid_for(a.B, 64);
   // y is stored as float when it is exactly a member value (odd-E median of f32)
-  const bool y32 = f32 && a.median && (a.E == 3 || a.E == 5);
+  const bool y32 = yev ? a.dtype == EKS_YEV32 : (f32 && a.median && (a.E == 3 || a.E == 5));
+  if (yev) {
+    p.ysrc = (const char *)a.obs;
+    p.evsrc = p.ysrc + yev_ev_offset(a.B, a.T, N, y32 ? sizeof(float) : sizeof(double));
+  } else {
+    p.ysrc = a.ws + p.y_off;
+    p.evsrc = a.ws + p.ev_off;
+  }
   auto run = [&](auto tag, auto ytag, auto unitag) -> int {
     using Tp = decltype(tag);
     using YT = decltype(ytag);
     constexpr bool U = decltype(unitag)::value;
     constexpr int LS = sub_len_c(R, N);
-    int rc = dispatch_members_c(a.E, [&](auto Ec) {
+    auto k1 = [&](auto Ec) {
       constexpr int EE = decltype(Ec)::value;
       prof_call_begin();
       prof_mark(a.stream, "k_c1_elem");
       hipLaunchKernelGGL((k_c1_elem<R, N, EE, Tp, YT, AI, CI, U>), dim3(gch), dim3(kBlock), 0,
                          a.stream, a, p);
       return check_launch("k_c1_elem");
-    });
+    };
+    int rc;
+    if constexpr (is_yev<Tp>::value)
+      rc = k1(ic<0>{});  // the members are not read: E does not matter
+    else
+      rc = dispatch_members_c(a.E, k1);
     if (rc) return rc;
     // the chunk scans: one lane per trajectory while the chain is short, one
     // wave per trajectory (log-depth scan) when it is long
@@ -1146,6 +1251,7 @@ int launch_shape(const SmoothArgs &a, int algo, long long L) {
   auto with_uni = [&](auto tag, auto ytag) -> int {
     return uni ? run(tag, ytag, std::true_type{}) : run(tag, ytag, std::false_type{});
   };
+  if (yev) return y32 ? with_uni(YevIn<float>{}, float{}) : with_uni(YevIn<double>{}, double{});
   if (y32) return with_uni(float{}, float{});
   return f32 ? with_uni(float{}, double{}) : with_uni(double{}, double{});
 }

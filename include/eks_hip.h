@@ -56,6 +56,10 @@ enum { EKS_STATUS_SINGULAR = 1, EKS_STATUS_BAD_MODEL = 2, EKS_STATUS_SCAN = 4 };
 enum { EKS_MODEL_A_IDENTITY = 1, EKS_MODEL_C_IDENTITY = 2 };
 
 enum { EKS_F32 = 0, EKS_F64 = 1 };
+/* eks_smooth input that is not member predictions but the ensemble output
+ * itself, as written by eks_fit (yev != NULL): y / ev planes, y float32
+ * (EKS_YEV32) or float64 (EKS_YEV64); see eks_yev_bytes. */
+enum { EKS_YEV32 = 2, EKS_YEV64 = 3 };
 enum { EKS_MEDIAN = 0, EKS_MEAN = 1 };
 
 /* Last error message of the calling thread ("" if none). */
@@ -211,7 +215,21 @@ size_t eks_fit_workspace_bytes(int64_t B, int64_t T, int n);
 int eks_fit(const void *obs, int obs_dtype, int64_t B, int64_t T, int E, int n, int r,
             int64_t sb, int64_t st, int64_t se, int64_t sj, int mode, int kind,
             double smooth_param, double quantile_keep, double *params, void *workspace,
-            size_t workspace_bytes, int32_t *status, void *stream);
+            size_t workspace_bytes, int32_t *status, void *yev, void *stream);
+
+/*
+ * Ensemble hand-off from eks_fit to eks_smooth (fit + smooth reading the
+ * member predictions once): with yev != NULL (eks_yev_bytes(B, T, n,
+ * obs_dtype, E, mode) bytes of device memory) eks_fit also writes the
+ * ensemble output -- y planes [t*n + j][b] (float32 when every y is a member
+ * value: float32 members, median, E in {3, 5}; else float64), then ev planes
+ * (float64) at a 256-byte aligned offset -- and eks_smooth called with
+ * obs = yev and obs_dtype = eks_yev_dtype(obs_dtype, E, mode)
+ * (EKS_YEV32 / EKS_YEV64; strides ignored) smooths from it.  Results are
+ * bit-identical to eks_smooth on the members.
+ */
+int eks_yev_dtype(int obs_dtype, int E, int mode);
+size_t eks_yev_bytes(int64_t B, int64_t T, int n, int obs_dtype, int E, int mode);
 
 /*
  * eks_interp1d -- linear resampling for the asynchronous two-camera paw

@@ -662,3 +662,32 @@ def test_torch_ops_match_batch_api(torch):
     assert p.shape == (4, 400, 2)
     nll = torch.ops.eks.nll(obs, params, 2, 2, "median", 0)
     assert torch.allclose(nll, batch.nll(obs, params, n=2, r=2), rtol=1e-12)
+
+
+# -------------------------------------------------------------------------
+# fit -> smooth ensemble hand-off (EKS_YEV32 / EKS_YEV64): bit-identical
+@pytest.mark.parametrize("kind,V,E,dtype,mode,algo", [
+    ("singleview", 1, 5, "f32", "median", 0), ("singleview", 1, 5, "f32", "median", 1),
+    ("singleview", 1, 4, "f64", "median", 2), ("singleview", 1, 3, "f32", "mean", 0),
+    ("multicam", 4, 5, "f32", "median", 0), ("multicam", 2, 3, "f64", "median", 1)])
+def test_fit_yev_handoff_bit_exact(torch, kind, V, E, dtype, mode, algo):
+    from eks_amd import batch, synthetic
+    rng = np.random.default_rng(E * V + algo)
+    K, T = 40, 3000
+    if kind == "singleview":
+        st = np.stack([synthetic.singleview_obs(rng, E, T)[:, :, 0] for _ in range(K)])
+        n, r = 2, 2
+    else:
+        st = synthetic.multiview_obs(rng, V, E, T, K=K).transpose(2, 0, 1, 3)
+        n, r = 2 * V, 3
+    st = np.ascontiguousarray(st, dtype=np.float32 if dtype == "f32" else np.float64)
+    obs = torch.from_numpy(st).cuda().permute(0, 2, 1, 3)   # (K, T, E, n)
+    kw = dict(kind=kind, n=n, r=r, smooth_param=0.01, quantile_keep=25, mode=mode)
+    p0, _ = batch.fit(obs, **kw)
+    p1, _, yev = batch.fit(obs, keep_yev=True, **kw)
+    assert torch.equal(p0, p1)
+    a = batch.smooth(obs, p0, n=n, r=r, mode=mode, algo=algo, check=True)["out"]
+    b = batch.smooth(yev, p1, n=n, r=r, mode=mode, algo=algo, check=True)["out"]
+    assert torch.equal(a, b)
+    y32 = dtype == "f32" and mode == "median" and E in (3, 5)
+    assert yev.code == (2 if y32 else 3)
