@@ -1,0 +1,71 @@
+"""Parity at BASELINE.json's full config-4 size (1024 videos x 17 keypoints
+x 5 members x 10 000 frames, 1.74e8 keypoint-timesteps) through properties
+that do not need the CPU oracle (which would take hours at this size):
+
+* the time-parallel algorithm (algo 2, 16 chunks per trajectory) equals the
+  sequential recursion (algo 1) on every trajectory (max|d| < 1e-8 px);
+* translation equivariance: shifting every member by (dx, dy) shifts the
+  model offsets and the smoothed outputs by exactly that (to rounding);
+* the device fit + hand-off path equals fit + smooth on the members.
+The CPU oracle itself is compared on a sample of this workload by bench.py
+(`max_abs_diff_vs_cpu`)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def work():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import bench
+    from eks_amd import batch
+    K, E, T = 17, 5, 10000
+    obs_tm = bench.gen_videos(torch, range(1024), K, E, T, 4, torch.device("cuda"))
+    obs = obs_tm.permute(3, 0, 1, 2)                            # (B, T, E, 2) view
+    params, _ = batch.fit(obs, kind="singleview", n=2, r=2, smooth_param=0.01,
+                          quantile_keep=25)
+    return torch, obs_tm, obs, params
+
+
+def test_algo2_equals_sequential_full_size(work):
+    torch, _, obs, params = work
+    from eks_amd import _lib, batch
+    flags = _lib.EKS_MODEL_A_IDENTITY | _lib.EKS_MODEL_C_IDENTITY
+    a2 = batch.smooth(obs, params, n=2, r=2, algo=2, flags=flags, check=True)["out"]
+    assert _lib.load().eks_smooth_chunk_len(obs.shape[0], obs.shape[1], 2) > 0
+    a1 = batch.smooth(obs, params, n=2, r=2, algo=1, flags=flags, check=True)["out"]
+    d = (a2 - a1).abs().max().item()
+    assert d < 1e-8, d
+
+
+def test_translation_equivariance(work):
+    torch, obs_tm, _, _ = work
+    from eks_amd import _lib, batch
+    B = 256 * 17
+    x = obs_tm[..., :B].to(torch.float64)                       # (T, E, 2, B), exact copy
+    shift = torch.tensor([64.0, -32.0], dtype=torch.float64, device=x.device)
+    xs = x + shift[None, None, :, None]                         # exact in float64
+    flags = _lib.EKS_MODEL_A_IDENTITY | _lib.EKS_MODEL_C_IDENTITY
+    outs, offs = [], []
+    for v in (x, xs):
+        o = v.permute(3, 0, 1, 2)
+        p, _ = batch.fit(o, kind="singleview", n=2, r=2, smooth_param=0.01, quantile_keep=25)
+        outs.append(batch.smooth(o, p, n=2, r=2, flags=flags, check=True)["out"])
+        offs.append(p[:, -2:])
+    assert (offs[1] - offs[0] - shift).abs().max().item() < 1e-9
+    assert (outs[1] - outs[0] - shift).abs().max().item() < 1e-8
+
+
+def test_handoff_full_size(work):
+    torch, _, obs, params = work
+    from eks_amd import _lib, batch
+    flags = _lib.EKS_MODEL_A_IDENTITY | _lib.EKS_MODEL_C_IDENTITY
+    p1, _, yev = batch.fit(obs, kind="singleview", n=2, r=2, smooth_param=0.01,
+                           quantile_keep=25, keep_yev=True)
+    assert torch.equal(p1, params)
+    a = batch.smooth(obs, params, n=2, r=2, flags=flags)["out"]
+    b = batch.smooth(yev, p1, n=2, r=2, flags=flags)["out"]
+    assert torch.equal(a, b)
