@@ -209,7 +209,7 @@ def workload_singleview(torch, a, dev, rank, world, config):
                          trajectories_per_rank=B, smooth_param=a.smooth_param,
                          quantile_keep=a.quantile_keep),
                 key=f"config{config}-singleview-v{len(videos) * world if config == 4 else 1}"
-                    f"-k{K}-e{E}-t{T}-n{world}-{a.scaling}",
+                    f"-k{K}-e{E}-t{T}-n{world}-{a.scaling}-a{a.algo}",
                 out=out, videos=videos)
 
 
@@ -259,7 +259,7 @@ def workload_multiview(torch, a, dev, rank, world):
                 units=K * T, bytes_per_unit=E * n * 4 + n * 8, cpu=cpu, cpu_default=5, desc=desc,
                 cfg=dict(cameras=V, keypoints=K, members=E, frames=T,
                          smooth_param=a.smooth_param, quantile_keep=a.quantile_keep),
-                key=f"config3-multiview-k{K}-e{E}-t{T}-n{world}")
+                key=f"config3-multiview-k{K}-e{E}-t{T}-n{world}-a{a.algo}")
 
 
 def workload_pupil(torch, a, dev, rank, world):
@@ -320,7 +320,7 @@ def workload_pupil(torch, a, dev, rank, world):
     return dict(step=step, status=status, units=4 * T, bytes_per_unit=(32 * E + 88) / 4,
                 cpu=cpu, cpu_default=1, desc=desc,
                 cfg=dict(frames=T, keypoints=4, members=E, candidates=len(cands)),
-                key=f"config5-pupil-t{T}-n{world}", extra=lambda: dict(
+                key=f"config5-pupil-t{T}-n{world}-a{a.algo}", extra=lambda: dict(
                     sweep_candidates=len(cands),
                     best_model=[float(x) for x in np.diag(cands[int(state['best'])]['A'])]))
 

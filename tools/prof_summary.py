@@ -1,6 +1,6 @@
 """Summarise a tools/gpu_profile.sh run into profiles/<tag>/.
 
-    python tools/prof_summary.py gpurun_out/prof_r01 profiles/r01 [workload_key]
+    python tools/prof_summary.py gpurun_out/prof_r01 profiles/r01 [workload_key, e.g. config4-singleview-v1024-k17-e5-t10000-n1-strong-a0]
 
 Reads the rocprofv3 kernel-stats CSV and the FETCH_SIZE / WRITE_SIZE counter
 CSVs (separate passes), keeps the EKS kernels, and writes
@@ -22,6 +22,7 @@ from collections import defaultdict
 
 
 def short(name: str) -> str:
+    name = name.replace("(anonymous namespace)::", "")
     base = name.split("(")[0].replace("void ", "")
     return base.strip()
 
@@ -60,7 +61,9 @@ def main(src: str, dst: str, key: str | None = None):
         if "avg_ms" in d and d["avg_ms"] > 0:
             d["hbm_GBps"] = b / (d["avg_ms"] * 1e-3) / 1e9
         summary["kernels"][k] = d
-        if "k_c" in k or "k_smooth_seq" in k:  # the eks_smooth pipeline (not setup kernels)
+        # the eks_smooth pipeline on member predictions (not the fit, not the
+        # hand-off variant of K1 the bench's end-to-end loop runs)
+        if ("k_c" in k or "k_smooth_seq" in k) and "YevIn" not in k:
             tot_bytes += b
             tot_ms += d.get("avg_ms", 0.0)
     summary["per_call"] = {"hbm_bytes": tot_bytes, "kernel_ms": tot_ms,
