@@ -68,6 +68,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--gather", action="store_true",
                     help="config 4: after timing, gather all outputs to rank 0 (RCCL) once")
+    ap.add_argument("--no-graph", action="store_true",
+                    help="launch every step eagerly instead of replaying a captured HIP graph")
     ap.add_argument("--scaling", choices=["strong", "weak"], default="strong",
                     help="config 4: strong = the video batch is split over ranks; weak = "
                          "every rank smooths --videos videos")
@@ -364,6 +366,25 @@ def main():
     torch.cuda.synchronize()
     if int((w["status"] != 0).sum().item()) != 0:
         raise RuntimeError("singular / mis-flagged trajectories in the bench workload")
+    # the step's kernel sequence captured once as a HIP graph (hipGraph via
+    # torch.cuda.CUDAGraph: the C ABI launches on the capturing stream and
+    # allocates nothing), replayed in the timed loop; eager launches if the
+    # capture is refused
+    graph = None
+    if not a.no_graph:
+        try:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                step()
+            g.replay()
+            torch.cuda.synchronize()
+            graph = g
+        except Exception as exc:  # pragma: no cover - depends on the runtime
+            print(f"[bench] HIP graph capture failed ({exc}); launching eagerly",
+                  file=sys.stderr)
+    eager_step = step
+    if graph is not None:
+        step = graph.replay
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -378,7 +399,7 @@ def main():
     # so the events do not perturb the timed loop above)
     _lib.profile_begin(4 * a.steps)
     for _ in range(a.steps):
-        step()
+        eager_step()
     kernels = [(n, ms / a.steps) for n, ms in _lib.profile_end()]  # per step
     kern_ms = sum(ms for _, ms in kernels)
     kern_ms_max = dist.max_over_ranks(kern_ms, device=dev)
@@ -474,6 +495,7 @@ def main():
             "max_abs_diff_vs_cpu": maxdiff,
             "end_to_end": None if e2e is None else dict(e2e, cpu_value=cpu_e2e),
             "setup_s": round(setup_s, 2),
+            "hip_graph": graph is not None,
         }
         if "extra" in w:
             line.update(w["extra"]())
