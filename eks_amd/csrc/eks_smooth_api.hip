@@ -39,13 +39,15 @@ size_t eks_smooth_workspace_bytes(int64_t B, int64_t T, int n, int r, int E, int
   return make_plan(B, T, r, n, chunk_len(B, T, r)).total;
 }
 
-int eks_smooth(const void *obs, int obs_dtype, int64_t B, int64_t T, int E, int n, int r,
-               int64_t sb, int64_t st, int64_t se, int64_t sj, int mode, const double *params,
-               double *out, int64_t ob, int64_t ot, int64_t oj, double *ms, double *nll,
-               void *workspace, size_t workspace_bytes, int model_flags, int algo,
-               int32_t *status, void *stream) {
+// shared validation and dispatch of eks_smooth / eks_smooth_seg
+static int smooth_call(const void *obs, int obs_dtype, int64_t B, int64_t T, int E, int n, int r,
+                       int64_t sb, int64_t st, int64_t se, int64_t sj, int mode,
+                       const double *params, double *out, int64_t ob, int64_t ot, int64_t oj,
+                       double *ms, double *nll, void *workspace, size_t workspace_bytes,
+                       int model_flags, int algo, int32_t *status, void *stream, int64_t t_base,
+                       int64_t T_total, int phase, const double *seg_in, double *seg_out) {
   if (!obs || !params || !status) return set_err(EKS_ERR_ARG, "eks_smooth: NULL pointer");
-  if (!out && (!nll || ms))
+  if (!out && (!nll || ms) && (phase == 0 || phase == 3))
     return set_err(EKS_ERR_ARG, "eks_smooth: out may be NULL only for a filter-only (nll) call");
   if (B < 0 || T < 1 || E < 1) return set_err(EKS_ERR_ARG, "eks_smooth: need B>=0, T>=1, E>=1");
   if (E > kMaxMembers) return set_err(EKS_ERR_UNSUPPORTED, "eks_smooth: E=%d > %d", E, kMaxMembers);
@@ -61,21 +63,84 @@ int eks_smooth(const void *obs, int obs_dtype, int64_t B, int64_t T, int E, int 
   if ((model_flags & EKS_MODEL_C_IDENTITY) && r != n)
     return set_err(EKS_ERR_ARG, "eks_smooth: C = I needs r == n");
   if (B == 0) return EKS_OK;
-  const int al = pick_algo(B, T, r, algo);
-  const size_t need = eks_smooth_workspace_bytes(B, T, n, r, E, al);
+  const int al = phase ? 2 : pick_algo(B, T, r, algo);
+  const size_t need = phase ? make_plan(B, T, r, n, chunk_len(B, T, r)).total
+                            : eks_smooth_workspace_bytes(B, T, n, r, E, al);
   if (!workspace || workspace_bytes < need)
     return set_err(EKS_ERR_ARG, "eks_smooth: workspace of %zu bytes needed", need);
   hipStream_t s = (hipStream_t)stream;
-  if (hipMemsetAsync(status, 0, (size_t)B * sizeof(int32_t), s) != hipSuccess)
+  if (phase <= 1 && hipMemsetAsync(status, 0, (size_t)B * sizeof(int32_t), s) != hipSuccess)
     return set_err(EKS_ERR_HIP, "eks_smooth: hipMemsetAsync(status) failed");
   SmoothArgs a{obs,    obs_dtype, B,  T,  E,         n,     r,  sb,      st,    se,
                sj,     mode == EKS_MEDIAN ? 1 : 0,  params, out, ob, ot, oj, ms,    nll,
                (char *)workspace, workspace_bytes, model_flags, al, status, s};
-  const long long L = chunk_len(B, T, r);
+  a.t_base = t_base;
+  a.T_total = T_total;
+  a.phase = phase;
+  a.seg_in = seg_in;
+  a.seg_out = seg_out;
+  long long L = chunk_len(B, T, r);
+  if (L >= T) L = (T + 7) / 8 * 8;
   if (r == 2 && n == 2) return launch_22(a, al, L);
   if (n == 4) return launch_34(a, al, L);
   if (n == 6) return launch_36(a, al, L);
   return launch_38(a, al, L);
+}
+
+int eks_smooth(const void *obs, int obs_dtype, int64_t B, int64_t T, int E, int n, int r,
+               int64_t sb, int64_t st, int64_t se, int64_t sj, int mode, const double *params,
+               double *out, int64_t ob, int64_t ot, int64_t oj, double *ms, double *nll,
+               void *workspace, size_t workspace_bytes, int model_flags, int algo,
+               int32_t *status, void *stream) {
+  clear_err();
+  return smooth_call(obs, obs_dtype, B, T, E, n, r, sb, st, se, sj, mode, params, out, ob, ot,
+                     oj, ms, nll, workspace, workspace_bytes, model_flags, algo, status, stream,
+                     0, T, 0, nullptr, nullptr);
+}
+
+size_t eks_smooth_seg_workspace_bytes(int64_t B, int64_t T, int n, int r) {
+  if (B <= 0 || T <= 0 || r < 1 || n < 1) return 0;
+  return make_plan(B, T, r, n, chunk_len(B, T, r)).total;
+}
+
+int eks_smooth_seg(const void *obs, int obs_dtype, int64_t B, int64_t T, int E, int n, int r,
+                   int64_t sb, int64_t st, int64_t se, int64_t sj, int mode,
+                   const double *params, double *out, int64_t ob, int64_t ot, int64_t oj,
+                   double *nll, void *workspace, size_t workspace_bytes, int model_flags,
+                   int32_t *status, int64_t t_base, int64_t T_total, int phase,
+                   const double *seg_in, double *seg_out, void *stream) {
+  clear_err();
+  if (phase < 1 || phase > 3) return set_err(EKS_ERR_ARG, "eks_smooth_seg: phase must be 1..3");
+  if (t_base < 0 || t_base + T > T_total)
+    return set_err(EKS_ERR_ARG, "eks_smooth_seg: frames [%lld, %lld) outside [0, %lld)",
+                   (long long)t_base, (long long)(t_base + T), (long long)T_total);
+  if (phase != 3 && !seg_out) return set_err(EKS_ERR_ARG, "eks_smooth_seg: seg_out needed");
+  if (phase == 2 && t_base > 0 && !seg_in)
+    return set_err(EKS_ERR_ARG, "eks_smooth_seg: phase 2 of a later segment needs the state");
+  if (phase == 3 && t_base + T < T_total && !seg_in)
+    return set_err(EKS_ERR_ARG, "eks_smooth_seg: phase 3 of an earlier segment needs the mean");
+  if (phase != 1 && !out) return set_err(EKS_ERR_ARG, "eks_smooth_seg: phases 2 and 3 need out");
+  return smooth_call(obs, obs_dtype, B, T, E, n, r, sb, st, se, sj, mode, params, out, ob, ot,
+                     oj, nullptr, nll, workspace, workspace_bytes, model_flags, 2, status,
+                     stream, t_base, T_total, phase,
+                     phase == 2 && t_base == 0 ? nullptr
+                     : (phase == 3 && t_base + T == T_total ? nullptr : seg_in),
+                     seg_out);
+}
+
+int eks_seg_combine(int kind, int64_t B, int nseg, int self, int r, const double *in,
+                    double *out, int32_t *status, void *stream) {
+  clear_err();
+  if (!in || !out) return set_err(EKS_ERR_ARG, "eks_seg_combine: NULL pointer");
+  if (kind != 0 && kind != 1) return set_err(EKS_ERR_ARG, "eks_seg_combine: kind 0 or 1");
+  if (nseg < 1 || self < 0 || self >= nseg) return set_err(EKS_ERR_ARG, "eks_seg_combine: bad self");
+  if (B <= 0) return EKS_OK;
+  hipStream_t s = (hipStream_t)stream;
+  switch (r) {
+    case 2: return launch_seg_combine<2>(kind, B, nseg, self, in, out, status, s);
+    case 3: return launch_seg_combine<3>(kind, B, nseg, self, in, out, status, s);
+    default: return set_err(EKS_ERR_UNSUPPORTED, "eks_seg_combine: r=%d not compiled in", r);
+  }
 }
 
 }  // extern "C"

@@ -64,6 +64,13 @@ struct SmoothArgs {
   int algo;
   int32_t *status;
   hipStream_t stream;
+  // time-sharded smoothing (eks_smooth_seg): this call covers global frames
+  // [t_base, t_base + T) of trajectories T_total long; phase 0 = whole
+  // pipeline, 1 / 2 / 3 = the three per-segment phases
+  long long t_base = 0, T_total = 0;
+  int phase = 0;
+  const double *seg_in = nullptr;
+  double *seg_out = nullptr;
 };
 
 // Target number of (chunk, trajectory) lanes: enough 256-thread blocks that
@@ -560,12 +567,13 @@ __global__ __launch_bounds__(kBlock) void k_c1_elem(SmoothArgs a, ChunkPlan p) {
   const long long c = ln.c;
   const unsigned b = ln.b;
   Model<R, N> md;
-  md.load(a.params + (long long)b * ParamLayout<R, N>::len, c == 0);
+  const bool first = c == 0 && a.t_base == 0;  // the globally first chunk starts at the prior
+  md.load(a.params + (long long)b * ParamLayout<R, N>::len, first);
   const long long s = c * p.L, e = min(TT, s + p.L);
   bool ok = true;
   Elem<R> El;
-  if (c == 0) {
-    if (!md.template valid<AI, CI>()) flag(a.status, b, EKS_STATUS_BAD_MODEL);
+  if (c == 0 && !md.template valid<AI, CI>()) flag(a.status, b, EKS_STATUS_BAD_MODEL);
+  if (first) {
     // chunk 0: the plain filter from the prior; summarised as the known
     // filtered state (Ab = 0, bb = m, Cb = P, no likelihood terms)
     double m[R], P[R][R];
@@ -599,7 +607,7 @@ __global__ __launch_bounds__(kBlock) void k_c1_elem(SmoothArgs a, ChunkPlan p) {
     });
   }
   El.store((double *)(a.ws + p.elem_off) + ((long long)b * p.NC + c) * Elem<R>::len, 1);
-  if (!ok) flag(a.status, b, c == 0 ? EKS_STATUS_SINGULAR : EKS_STATUS_SCAN);
+  if (!ok) flag(a.status, b, first ? EKS_STATUS_SINGULAR : EKS_STATUS_SCAN);
 }
 
 template <int R, int N>
@@ -611,24 +619,31 @@ __global__ __launch_bounds__(64) void k_c2_fscan(SmoothArgs a, ChunkPlan p) {
   const double *elem = (const double *)(a.ws + p.elem_off);
   double *cst = (double *)(a.ws + p.cstart_off);
   double m[R], P[R][R];
-  {
+  Elem<R> El, Nx;
+  // elements are stored trajectory-major: row (b, c) of Elem<R>::len doubles
+  const double *erow = elem + b * p.NC * Elem<R>::len;
+  bool ok = true;
+  if (a.t_base == 0) {
     using L = ParamLayout<R, N>;
     const double *pp = a.params + b * L::len;
     load_vec<R>(pp + L::m0, m);
     load_mat<R, R>(pp + L::S0, P);
     store_state<R>(cst + b, B, m, P);  // chunk 0 starts from the prior
-  }
-  Elem<R> El, Nx;
-  // elements are stored trajectory-major: row (b, c) of Elem<R>::len doubles
-  const double *erow = elem + b * p.NC * Elem<R>::len;
-  El.load(erow, 1);
+    El.load(erow, 1);
 #pragma unroll
-  for (int i = 0; i < R; ++i) {
-    m[i] = El.bb[i];
+    for (int i = 0; i < R; ++i) {
+      m[i] = El.bb[i];
 #pragma unroll
-    for (int j = 0; j < R; ++j) P[i][j] = El.Cb[i][j];
+      for (int j = 0; j < R; ++j) P[i][j] = El.Cb[i][j];
+    }
+  } else {
+    // a later time segment: chunk 0 starts from the filtered state handed
+    // over by the earlier segments, and its element is a regular one
+    load_state<R>(a.seg_in + b * (R + Sym<R>::len), 1, m, P);
+    store_state<R>(cst + b, B, m, P);
+    El.load(erow, 1);
+    ok = compose_state<R>(m, P, El) && ok;
   }
-  bool ok = true;
   // software pipelined: the element of chunk c+1 is in flight while chunk c
   // is composed (the chain is latency bound, not bandwidth bound)
   if (p.NC > 1) El.load(erow + Elem<R>::len, 1);
@@ -703,7 +718,21 @@ __global__ __launch_bounds__(64 * W) void k_c2_fscan_w(SmoothArgs a, ChunkPlan p
       }
     }
   }
-  if (c0 < c1) {
+  if (c0 < c1 && a.t_base > 0) {
+    // a later time segment: every thread starts from the handed-over state
+    // composed with the elements before its first chunk
+    double m[R], P[R][R];
+    load_state<R>(a.seg_in + b * (R + Sym<R>::len), 1, m, P);
+    if (tid > 0) ok = compose_state<R>(m, P, ex) && ok;
+    for (long long c = c0; c < c1; ++c) {
+      store_state<R>(cst + (c * KS) * B + b, B, m, P);
+      if (c + 1 < c1) {
+        Elem<R> e;
+        e.load(elem + (b * NC + c) * Elem<R>::len, 1);
+        ok = compose_state<R>(m, P, e) && ok;
+      }
+    }
+  } else if (c0 < c1) {
     double m[R], P[R][R];
     long long c = c0;
     if (tid == 0) {
@@ -831,10 +860,18 @@ __global__ __launch_bounds__(64 * W) void k_c4_bscan_w(SmoothArgs a, ChunkPlan p
     }
   }
   double ms[R];
+  // X maps the value entering the last chunk (none for the globally last
+  // segment: its map is constant; the next segment's ms otherwise)
 #pragma unroll
-  for (int i = 0; i < R; ++i) ms[i] = X.g[i];
+  for (int i = 0; i < R; ++i) {
+    double t = X.g[i];
+    if (a.seg_in)
+#pragma unroll
+      for (int k = 0; k < R; ++k) t = fma(X.G[i][k], a.seg_in[b * R + k], t);
+    ms[i] = t;
+  }
   for (long long c = c1 - 1; c >= c0; --c) {
-    if (c + 1 < NC) {
+    if (c + 1 < NC || a.seg_in) {
 #pragma unroll
       for (int i = 0; i < R; ++i) msend[(c * R + i) * B + b] = ms[i];
     }
@@ -868,6 +905,134 @@ __global__ __launch_bounds__(64 * W) void k_c4_bscan_w(SmoothArgs a, ChunkPlan p
       if (l == 0) a.nll[b] = s;
     }
   }
+}
+
+// Time-sharded smoothing (eks_smooth_seg): the aggregate of a segment's
+// chunk elements (phase 1) and of its chunk RTS maps (phase 2), one wave per
+// trajectory, lanes composing contiguous chunk ranges then an ordered
+// in-wave scan.  Elements compose left to right, maps right to left.
+template <int R>
+__global__ __launch_bounds__(64) void k_seg_elems(SmoothArgs a, ChunkPlan p) {
+  const long long b = blockIdx.x;
+  const int l = threadIdx.x;
+  const long long NC = p.NC;
+  if (b >= a.B) return;
+  const double *elem = (const double *)(a.ws + p.elem_off);
+  const long long q = (NC + 63) / 64;
+  const long long c0 = min(NC, (long long)l * q), c1 = min(NC, c0 + q);
+  bool ok = true;
+  Elem<R> agg;
+  agg.set_identity();
+  for (long long c = c0; c < c1; ++c) {
+    Elem<R> e, t;
+    e.load(elem + (b * NC + c) * Elem<R>::len, 1);
+    ok = compose_elem<R>(agg, e, t) && ok;
+    agg = t;
+  }
+#pragma unroll
+  for (int k = 1; k < 64; k <<= 1) {
+    const Elem<R> o = shfl_elem<R, true>(agg, k);
+    if (l >= k) {
+      Elem<R> t;
+      ok = compose_elem<R>(o, agg, t) && ok;
+      agg = t;
+    }
+  }
+  if (l == 63) agg.store(a.seg_out + b * Elem<R>::len, 1);
+  if (!ok) flag(a.status, b, EKS_STATUS_SCAN);
+}
+
+template <int R>
+__global__ __launch_bounds__(64) void k_seg_maps(SmoothArgs a, ChunkPlan p) {
+  const long long b = blockIdx.x;
+  const int l = threadIdx.x;
+  const long long NC = p.NC;
+  if (b >= a.B) return;
+  const double *bw = (const double *)(a.ws + p.bwd_off);
+  const long long q = (NC + 63) / 64;
+  const long long c0 = min(NC, (long long)l * q), c1 = min(NC, c0 + q);
+  Affine<R> F;
+  F.set_identity();
+  for (long long c = c1 - 1; c >= c0; --c) {
+    Affine<R> f;
+    const double *sp = bw + (b * NC + c) * (R * R + R);
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      f.g[i] = sp[R * R + i];
+#pragma unroll
+      for (int j = 0; j < R; ++j) f.G[i][j] = sp[i * R + j];
+    }
+    F = f.after(F);
+  }
+#pragma unroll
+  for (int k = 1; k < 64; k <<= 1) {
+    const Affine<R> o = F.shfl_down(k);
+    if (l + k < 64) F = F.after(o);
+  }
+  if (l == 0) {
+    double *o = a.seg_out + b * (R * R + R);
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      o[R * R + i] = F.g[i];
+#pragma unroll
+      for (int j = 0; j < R; ++j) o[i * R + j] = F.G[i][j];
+    }
+  }
+}
+
+// Combine the all-gathered segment aggregates of every rank (one thread per
+// trajectory).  kind 0: the filtered state entering segment `self` = the
+// first segment's element (a state: Ab = 0) composed with the elements of
+// segments 1 .. self-1.  kind 1: the smoothed mean entering segment self + 1
+// = the maps of segments nseg-1 .. self+1 applied right to left (the last
+// segment's map is constant).
+template <int R>
+__global__ __launch_bounds__(64) void k_seg_combine(int kind, long long B, int nseg, int self,
+                                                    const double *__restrict__ in,
+                                                    double *__restrict__ out,
+                                                    int32_t *__restrict__ status) {
+  const long long b = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  bool ok = true;
+  if (kind == 0) {
+    constexpr int EL = Elem<R>::len;
+    Elem<R> e0;
+    e0.load(in + b * EL, 1);
+    double m[R], P[R][R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      m[i] = e0.bb[i];
+#pragma unroll
+      for (int j = 0; j < R; ++j) P[i][j] = e0.Cb[i][j];
+    }
+    for (int sg = 1; sg < self; ++sg) {
+      Elem<R> e;
+      e.load(in + ((long long)sg * B + b) * EL, 1);
+      ok = compose_state<R>(m, P, e) && ok;
+    }
+    store_state<R>(out + b * (R + Sym<R>::len), 1, m, P);
+  } else {
+    constexpr int ML = R * R + R;
+    double ms[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) ms[i] = 0.0;
+    for (int sg = nseg - 1; sg > self; --sg) {
+      const double *f = in + ((long long)sg * B + b) * ML;
+      double nx[R];
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        double t = f[R * R + i];
+#pragma unroll
+        for (int k = 0; k < R; ++k) t = fma(f[i * R + k], ms[k], t);
+        nx[i] = t;
+      }
+#pragma unroll
+      for (int i = 0; i < R; ++i) ms[i] = nx[i];
+    }
+#pragma unroll
+    for (int i = 0; i < R; ++i) out[b * R + i] = ms[i];
+  }
+  if (!ok && status) atomicOr(status + b, EKS_STATUS_SCAN);
 }
 
 // y / ev of step t (time-major planes), raw
@@ -930,10 +1095,10 @@ __global__ __launch_bounds__(kBlock) void k_c3_rerun(SmoothArgs a, ChunkPlan p) 
         }
         if (t + D < e)
           load_yev<N, YT>(ybuf, evbuf, t + D, p.yB, p.ylane(b), yr[q % D], er[q % D]);
-        if (t > 0) kf_predict<R, AI>(m, P, md.A, md.Q);
+        if (t + a.t_base > 0) kf_predict<R, AI>(m, P, md.A, md.Q);
         kf_update<R, N, CI>(m, P, md.C, y, rv, acc, ok);
         if (!p.smooth) continue;
-        if (t + 1 < TT) {
+        if (t + a.t_base + 1 < a.T_total) {
           double J[R][R], d[R], GJ[R][R];
           ok = rts_gain<R, AI>(m, P, md.A, md.Q, J, d) && ok;
 #pragma unroll
@@ -995,8 +1160,13 @@ __global__ __launch_bounds__(64) void k_c4_bscan(SmoothArgs a, ChunkPlan p) {
     }
   };
   double ms[R], G[R][R], g[R], Gn[R][R], gn[R];
+  // the value entering the last chunk: none for the globally last segment
+  // (its map is constant), the next segment's ms otherwise
 #pragma unroll
-  for (int i = 0; i < R; ++i) ms[i] = 0.0;
+  for (int i = 0; i < R; ++i) ms[i] = a.seg_in ? a.seg_in[b * R + i] : 0.0;
+  if (a.seg_in)
+#pragma unroll
+    for (int i = 0; i < R; ++i) msend[((p.NC - 1) * R + i) * B + b] = ms[i];
   load_map(p.NC - 1, G, g);
   for (long long c = p.NC - 1; c >= 0; --c) {
     if (c >= 1) load_map(c - 1, Gn, gn);  // next map in flight during this one
@@ -1057,7 +1227,10 @@ __global__ __launch_bounds__(kBlock) void k_c5_final(SmoothArgs a, ChunkPlan p) 
   const double *evbuf = (const double *)p.evsrc;
   const double *ckpt = (const double *)(a.ws + p.ckpt_off);
   double ms[R];
-  if (c + 1 < p.NC) {
+  // ms entering the chunk from the right: from K4, or for the globally last
+  // chunk unused (its map ends in the constant mf[T-1]); the last chunk of an
+  // earlier time segment gets it from the next segment (eks_smooth_seg)
+  if (c + 1 < p.NC || a.t_base + TT < a.T_total) {
     const double *me = (const double *)(a.ws + p.msend_off);
 #pragma unroll
     for (int i = 0; i < R; ++i) ms[i] = pl(me, c * R + i, B, b);
@@ -1090,9 +1263,9 @@ __global__ __launch_bounds__(kBlock) void k_c5_final(SmoothArgs a, ChunkPlan p) 
           y[q] = (double)yr[j][q] - md.off[q];
           rv[q] = er[j][q];
         }
-        if (t > 0) kf_predict<R, AI>(m, P, md.A, md.Q);
+        if (t + a.t_base > 0) kf_predict<R, AI>(m, P, md.A, md.Q);
         kf_update<R, N, CI>(m, P, md.C, y, rv, dummy, ok);
-        if (t + 1 < TT) {
+        if (t + a.t_base + 1 < a.T_total) {
           ok = rts_gain<R, AI>(m, P, md.A, md.Q, Jr[j], dr[j]) && ok;
         } else {
 #pragma unroll
@@ -1191,46 +1364,63 @@ int launch_shape(const SmoothArgs &a, int algo, long long L) {
     using YT = decltype(ytag);
     constexpr bool U = decltype(unitag)::value;
     constexpr int LS = sub_len_c(R, N);
-    auto k1 = [&](auto Ec) {
-      constexpr int EE = decltype(Ec)::value;
-      prof_call_begin();
-      prof_mark(a.stream, "k_c1_elem");
-      hipLaunchKernelGGL((k_c1_elem<R, N, EE, Tp, YT, AI, CI, U>), dim3(gch), dim3(kBlock), 0,
-                         a.stream, a, p);
-      return check_launch("k_c1_elem");
-    };
+    const int ph = a.phase;  // 0: whole pipeline; 1 / 2 / 3: time-segment phases
+    prof_call_begin();
     int rc;
-    if constexpr (is_yev<Tp>::value)
-      rc = k1(ic<0>{});  // the members are not read: E does not matter
-    else
-      rc = dispatch_members_c(a.E, k1);
-    if (rc) return rc;
+    if (ph == 0 || ph == 1) {
+      auto k1 = [&](auto Ec) {
+        constexpr int EE = decltype(Ec)::value;
+        prof_mark(a.stream, "k_c1_elem");
+        hipLaunchKernelGGL((k_c1_elem<R, N, EE, Tp, YT, AI, CI, U>), dim3(gch), dim3(kBlock), 0,
+                           a.stream, a, p);
+        return check_launch("k_c1_elem");
+      };
+      if constexpr (is_yev<Tp>::value)
+        rc = k1(ic<0>{});  // the members are not read: E does not matter
+      else
+        rc = dispatch_members_c(a.E, k1);
+      if (rc) return rc;
+      if (ph == 1) {  // the segment's aggregate element
+        prof_mark(a.stream, "k_seg_elems");
+        hipLaunchKernelGGL((k_seg_elems<R>), dim3((unsigned)a.B), dim3(64), 0, a.stream, a, p);
+        prof_call_end(a.stream);
+        return check_launch("k_seg_elems");
+      }
+    }
     // the chunk scans: one lane per trajectory while the chain is short, one
     // wave per trajectory (log-depth scan) when it is long
     const bool wave_scan = p.NC > wave_scan_chunks();
     const int sw = scan_waves(p.NC);
-    prof_mark(a.stream, "k_c2_fscan");
-    if (!wave_scan)
-      hipLaunchKernelGGL((k_c2_fscan<R, N>), dim3(g64), dim3(64), 0, a.stream, a, p);
-    else if (sw == 8)
-      hipLaunchKernelGGL((k_c2_fscan_w<R, N, 8>), dim3((unsigned)a.B), dim3(512), 0, a.stream,
-                         a, p);
-    else if (sw == 4)
-      hipLaunchKernelGGL((k_c2_fscan_w<R, N, 4>), dim3((unsigned)a.B), dim3(256), 0, a.stream,
-                         a, p);
-    else
-      hipLaunchKernelGGL((k_c2_fscan_w<R, N, 1>), dim3((unsigned)a.B), dim3(64), 0, a.stream, a,
-                         p);
-    if ((rc = check_launch("k_c2_fscan"))) return rc;
-    prof_mark(a.stream, "k_c3_rerun");
-    hipLaunchKernelGGL((k_c3_rerun<R, N, YT, AI, CI, LS, U>), dim3(gch), dim3(kBlock), 0,
-                       a.stream, a, p);
-    if ((rc = check_launch("k_c3_rerun"))) return rc;
-    if (!p.smooth) {  // filter only: sum the NLL shares, no backward pass
-      prof_mark(a.stream, "k_c4_nll");
-      hipLaunchKernelGGL((k_c4_nll<R>), dim3((unsigned)a.B), dim3(64), 0, a.stream, a, p);
-      prof_call_end(a.stream);
-      return check_launch("k_c4_nll");
+    if (ph == 0 || ph == 2) {
+      prof_mark(a.stream, "k_c2_fscan");
+      if (!wave_scan)
+        hipLaunchKernelGGL((k_c2_fscan<R, N>), dim3(g64), dim3(64), 0, a.stream, a, p);
+      else if (sw == 8)
+        hipLaunchKernelGGL((k_c2_fscan_w<R, N, 8>), dim3((unsigned)a.B), dim3(512), 0,
+                           a.stream, a, p);
+      else if (sw == 4)
+        hipLaunchKernelGGL((k_c2_fscan_w<R, N, 4>), dim3((unsigned)a.B), dim3(256), 0,
+                           a.stream, a, p);
+      else
+        hipLaunchKernelGGL((k_c2_fscan_w<R, N, 1>), dim3((unsigned)a.B), dim3(64), 0, a.stream,
+                           a, p);
+      if ((rc = check_launch("k_c2_fscan"))) return rc;
+      prof_mark(a.stream, "k_c3_rerun");
+      hipLaunchKernelGGL((k_c3_rerun<R, N, YT, AI, CI, LS, U>), dim3(gch), dim3(kBlock), 0,
+                         a.stream, a, p);
+      if ((rc = check_launch("k_c3_rerun"))) return rc;
+      if (ph == 2) {  // the segment's aggregate RTS map
+        prof_mark(a.stream, "k_seg_maps");
+        hipLaunchKernelGGL((k_seg_maps<R>), dim3((unsigned)a.B), dim3(64), 0, a.stream, a, p);
+        prof_call_end(a.stream);
+        return check_launch("k_seg_maps");
+      }
+      if (!p.smooth) {  // filter only: sum the NLL shares, no backward pass
+        prof_mark(a.stream, "k_c4_nll");
+        hipLaunchKernelGGL((k_c4_nll<R>), dim3((unsigned)a.B), dim3(64), 0, a.stream, a, p);
+        prof_call_end(a.stream);
+        return check_launch("k_c4_nll");
+      }
     }
     prof_mark(a.stream, "k_c4_bscan");
     if (!wave_scan)
@@ -1254,6 +1444,14 @@ int launch_shape(const SmoothArgs &a, int algo, long long L) {
   if (yev) return y32 ? with_uni(YevIn<float>{}, float{}) : with_uni(YevIn<double>{}, double{});
   if (y32) return with_uni(float{}, float{});
   return f32 ? with_uni(float{}, double{}) : with_uni(double{}, double{});
+}
+
+template <int R>
+int launch_seg_combine(int kind, long long B, int nseg, int self, const double *in, double *out,
+                       int32_t *status, hipStream_t s) {
+  hipLaunchKernelGGL((k_seg_combine<R>), dim3(grid_for(B, 64)), dim3(64), 0, s, kind, B, nseg,
+                     self, in, out, status);
+  return check_launch("k_seg_combine");
 }
 
 // per-shape entry points (defined in eks_shape_*.hip)

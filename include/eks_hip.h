@@ -179,6 +179,40 @@ int eks_smooth(const void *obs, int obs_dtype, int64_t B, int64_t T, int E, int 
 int64_t eks_smooth_chunk_len(int64_t B, int64_t T, int r);
 
 /*
+ * Time-sharded smoothing (SURVEY.md §8(e) "shard the time axis"): the frames
+ * of every trajectory are split into nseg contiguous segments, segment k on
+ * rank k, and the chunked scan of eks_smooth runs per segment in three
+ * phases with two exchanges of per-trajectory aggregates between them (the
+ * reference has no equivalent: its smoother is one sequential loop,
+ * eks/core.py:220-352).  Per segment of T frames starting at t_base of
+ * T_total, with the arguments of eks_smooth (obs/out point at the segment's
+ * own frames):
+ *   phase 1: seg_out (B, EL), EL = R*R + 2R + R(R+1) <- the segment's aggregate
+ *            filtering element (A, b, C, eta, J; C and J packed) (zeroes status);
+ *   -> all-gather the elements, eks_seg_combine(kind 0) -> state (B, R+R(R+1)/2)
+ *   phase 2: seg_in = that state (NULL on segment 0); seg_out (B, R*R + R) <-
+ *            the segment's aggregate smoothing map ms_in -> ms_first;
+ *   -> all-gather the maps, eks_seg_combine(kind 1) -> mean (B, R)
+ *   phase 3: seg_in = the smoothed mean entering the next segment (NULL on
+ *            the last); writes out (and nll = the segment's share, whose sum
+ *            over segments is eks_smooth's nll).
+ * The workspace (eks_smooth_seg_workspace_bytes) must survive phases 1..3.
+ * Results equal eks_smooth's to rounding (different association order).
+ */
+size_t eks_smooth_seg_workspace_bytes(int64_t B, int64_t T, int n, int r);
+int eks_smooth_seg(const void *obs, int obs_dtype, int64_t B, int64_t T, int E, int n, int r,
+                   int64_t sb, int64_t st, int64_t se, int64_t sj, int mode,
+                   const double *params, double *out, int64_t ob, int64_t ot, int64_t oj,
+                   double *nll, void *workspace, size_t workspace_bytes, int model_flags,
+                   int32_t *status, int64_t t_base, int64_t T_total, int phase,
+                   const double *seg_in, double *seg_out, void *stream);
+/* kind 0: in = nseg gathered elements (nseg, B, EL) -> out = state entering
+ * segment `self`; kind 1: in = gathered maps (nseg, B, R*R+R) -> out = mean
+ * entering segment self+1 (zeros when self is last).  status may be NULL. */
+int eks_seg_combine(int kind, int64_t B, int nseg, int self, int r, const double *in,
+                    double *out, int32_t *status, void *stream);
+
+/*
  * eks_newton_filter -- replaces eks/newton_eks.py:115-148
  * `kalman_newton_recursive(y, mu0, S0, A, B, ensemble_vars, E, max_iter)`
  * for B trajectories (one lane each): information-form filter with
