@@ -68,6 +68,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--gather", action="store_true",
                     help="config 4: after timing, gather all outputs to rank 0 (RCCL) once")
+    ap.add_argument("--timeshard", action="store_true",
+                    help="config 5: split the frames over the ranks (eks_amd.timeshard: two "
+                         "all_gathers of per-segment aggregates) instead of replicas")
     ap.add_argument("--no-graph", action="store_true",
                     help="launch every step eagerly instead of replaying a captured HIP graph")
     ap.add_argument("--scaling", choices=["strong", "weak"], default="strong",
@@ -291,6 +294,21 @@ def workload_pupil(torch, a, dev, rank, world):
     status = torch.empty((1,), dtype=torch.int32, device=dev)
     cands_obs = obs.expand(len(cands), -1, -1, -1)  # batch stride 0: members shared
     state = {}
+    t0, Tk = 0, T
+    if a.timeshard:
+        from eks_amd import timeshard
+        t0, Tk = timeshard.split_frames(T, world, rank)
+        seg_out = out[:, t0:t0 + Tk]
+
+    def step_timeshard():
+        scores = timeshard.smooth_time_sharded(cands_obs[:, t0:t0 + Tk], params, n=8, r=3,
+                                               t_base=t0, T_total=T, want_out=False)["nll"]
+        best = torch.argmin(scores)            # the same on every rank (summed NLL)
+        p_best = params.index_select(0, best.view(1)).contiguous()
+        r = timeshard.smooth_time_sharded(obs[:, t0:t0 + Tk], p_best, n=8, r=3, t_base=t0,
+                                          T_total=T, out=seg_out, want_ms=True)
+        state["best"], state["scores"], state["ms"] = best, scores, r["ms"]
+        status.copy_(r["status"])
 
     def step():
         scores = batch.nll(cands_obs, params, n=8, r=3, algo=a.algo, check=False)
@@ -319,10 +337,14 @@ def workload_pupil(torch, a, dev, rank, world):
     desc = (f"config 5: IBL-pupil smoother, {T} frames x 4 keypoints x {E} members (r=3 latent, "
             f"n=8): NLL sweep over {len(cands)} (diameter_s, com_s) models (filter-only, "
             f"batched) + smoothing of the argmin, float64")
-    return dict(step=step, status=status, units=4 * T, bytes_per_unit=(32 * E + 88) / 4,
-                cpu=cpu, cpu_default=1, desc=desc,
+    if a.timeshard:
+        desc += f"; frames split over {world} rank(s) (time-sharded scan)"
+    return dict(step=step_timeshard if a.timeshard else step, status=status, units=4 * Tk,
+                bytes_per_unit=(32 * E + 88) / 4, cpu=cpu, cpu_default=1, desc=desc,
+                timeshard=a.timeshard,
                 cfg=dict(frames=T, keypoints=4, members=E, candidates=len(cands)),
-                key=f"config5-pupil-t{T}-n{world}-a{a.algo}", extra=lambda: dict(
+                key=f"config5-pupil-t{T}-n{world}-a{a.algo}{'-ts' if a.timeshard else ''}",
+                extra=lambda: dict(
                     sweep_candidates=len(cands),
                     best_model=[float(x) for x in np.diag(cands[int(state['best'])]['A'])]))
 
@@ -371,7 +393,8 @@ def main():
     # allocates nothing), replayed in the timed loop; eager launches if the
     # capture is refused
     graph = None
-    if not a.no_graph:
+    # (a time-sharded step exchanges through host-side collectives: eager)
+    if not a.no_graph and not (w.get("timeshard") and world > 1):
         try:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
@@ -397,7 +420,7 @@ def main():
     # per-kernel launch durations: HIP events recorded by libeks_hip on the
     # launch stream around each kernel of each eks_smooth call (separate pass,
     # so the events do not perturb the timed loop above)
-    _lib.profile_begin(4 * a.steps)
+    _lib.profile_begin(8 * a.steps)
     for _ in range(a.steps):
         eager_step()
     kernels = [(n, ms / a.steps) for n, ms in _lib.profile_end()]  # per step
@@ -461,9 +484,11 @@ def main():
         value = units_total / elapsed_max * a.steps
         achieved = w["bytes_per_unit"] * units_local / (kern_ms_max * 1e-3) / 1e9
         pmc = load_pmc(w["key"])
-        scaling = "strong" if (a.config == 4 and a.scaling == "strong") else "weak"
+        scaling = ("strong" if (a.config == 4 and a.scaling == "strong") or w.get("timeshard")
+                   else "weak")
         par = (f"videos sharded over {world} rank(s), no data-path collective" if a.config == 4
-               else f"{world} independent replica(s)")
+               else f"frames split over {world} rank(s), 2 all_gathers of segment aggregates"
+               if w.get("timeshard") else f"{world} independent replica(s)")
         line = {
             "metric": METRIC,
             "value": value,

@@ -106,22 +106,26 @@ size_t eks_smooth_seg_workspace_bytes(int64_t B, int64_t T, int n, int r) {
 int eks_smooth_seg(const void *obs, int obs_dtype, int64_t B, int64_t T, int E, int n, int r,
                    int64_t sb, int64_t st, int64_t se, int64_t sj, int mode,
                    const double *params, double *out, int64_t ob, int64_t ot, int64_t oj,
-                   double *nll, void *workspace, size_t workspace_bytes, int model_flags,
-                   int32_t *status, int64_t t_base, int64_t T_total, int phase,
+                   double *ms, double *nll, void *workspace, size_t workspace_bytes,
+                   int model_flags, int32_t *status, int64_t t_base, int64_t T_total, int phase,
                    const double *seg_in, double *seg_out, void *stream) {
   clear_err();
   if (phase < 1 || phase > 3) return set_err(EKS_ERR_ARG, "eks_smooth_seg: phase must be 1..3");
   if (t_base < 0 || t_base + T > T_total)
     return set_err(EKS_ERR_ARG, "eks_smooth_seg: frames [%lld, %lld) outside [0, %lld)",
                    (long long)t_base, (long long)(t_base + T), (long long)T_total);
-  if (phase != 3 && !seg_out) return set_err(EKS_ERR_ARG, "eks_smooth_seg: seg_out needed");
+  if ((phase == 1 || (phase == 2 && out)) && !seg_out)
+    return set_err(EKS_ERR_ARG, "eks_smooth_seg: seg_out needed");
+  if (phase == 2 && !out && !nll)
+    return set_err(EKS_ERR_ARG, "eks_smooth_seg: phase 2 needs out (smooth) or nll (filter only)");
   if (phase == 2 && t_base > 0 && !seg_in)
     return set_err(EKS_ERR_ARG, "eks_smooth_seg: phase 2 of a later segment needs the state");
   if (phase == 3 && t_base + T < T_total && !seg_in)
     return set_err(EKS_ERR_ARG, "eks_smooth_seg: phase 3 of an earlier segment needs the mean");
-  if (phase != 1 && !out) return set_err(EKS_ERR_ARG, "eks_smooth_seg: phases 2 and 3 need out");
+  if (phase == 3 && !out) return set_err(EKS_ERR_ARG, "eks_smooth_seg: phase 3 needs out");
   return smooth_call(obs, obs_dtype, B, T, E, n, r, sb, st, se, sj, mode, params, out, ob, ot,
-                     oj, nullptr, nll, workspace, workspace_bytes, model_flags, 2, status,
+                     oj, phase == 3 ? ms : nullptr, nll, workspace, workspace_bytes,
+                     model_flags, 2, status,
                      stream, t_base, T_total, phase,
                      phase == 2 && t_base == 0 ? nullptr
                      : (phase == 3 && t_base + T == T_total ? nullptr : seg_in),

@@ -911,15 +911,20 @@ __global__ __launch_bounds__(64 * W) void k_c4_bscan_w(SmoothArgs a, ChunkPlan p
 // chunk elements (phase 1) and of its chunk RTS maps (phase 2), one wave per
 // trajectory, lanes composing contiguous chunk ranges then an ordered
 // in-wave scan.  Elements compose left to right, maps right to left.
-template <int R>
-__global__ __launch_bounds__(64) void k_seg_elems(SmoothArgs a, ChunkPlan p) {
+// Time segments, phase 1: the segment's aggregate filtering element = the
+// ordered composition of its chunk elements (one block of W waves per
+// trajectory: per-thread runs of chunks, an in-order tree over the lanes of
+// each wave, then the W wave totals in order).
+template <int R, int W>
+__global__ __launch_bounds__(64 * W) void k_seg_elems(SmoothArgs a, ChunkPlan p) {
+  __shared__ double tot[W][Elem<R>::len];
   const long long b = blockIdx.x;
-  const int l = threadIdx.x;
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
   const long long NC = p.NC;
   if (b >= a.B) return;
   const double *elem = (const double *)(a.ws + p.elem_off);
-  const long long q = (NC + 63) / 64;
-  const long long c0 = min(NC, (long long)l * q), c1 = min(NC, c0 + q);
+  const long long q = (NC + 64 * W - 1) / (64 * W);
+  const long long c0 = min(NC, (long long)tid * q), c1 = min(NC, c0 + q);
   bool ok = true;
   Elem<R> agg;
   agg.set_identity();
@@ -930,46 +935,69 @@ __global__ __launch_bounds__(64) void k_seg_elems(SmoothArgs a, ChunkPlan p) {
     agg = t;
   }
 #pragma unroll
-  for (int k = 1; k < 64; k <<= 1) {
-    const Elem<R> o = shfl_elem<R, true>(agg, k);
-    if (l >= k) {
+  for (int k = 1; k < 64; k <<= 1) {  // lane l: lanes [l, l + 2k) in order
+    const Elem<R> o = shfl_elem<R, false>(agg, k);
+    if (l + k < 64) {
       Elem<R> t;
-      ok = compose_elem<R>(o, agg, t) && ok;
+      ok = compose_elem<R>(agg, o, t) && ok;
       agg = t;
     }
   }
-  if (l == 63) agg.store(a.seg_out + b * Elem<R>::len, 1);
+  if (l == 0) agg.store(tot[w], 1);
+  __syncthreads();
+  if (tid == 0) {
+    for (int v = 1; v < W; ++v) {
+      Elem<R> e, t;
+      e.load(tot[v], 1);
+      ok = compose_elem<R>(agg, e, t) && ok;
+      agg = t;
+    }
+    agg.store(a.seg_out + b * Elem<R>::len, 1);
+  }
   if (!ok) flag(a.status, b, EKS_STATUS_SCAN);
 }
 
-template <int R>
-__global__ __launch_bounds__(64) void k_seg_maps(SmoothArgs a, ChunkPlan p) {
+// Time segments, phase 2: the segment's aggregate smoothing map (the chunk
+// maps composed right to left), same block shape as k_seg_elems.
+template <int R, int W>
+__global__ __launch_bounds__(64 * W) void k_seg_maps(SmoothArgs a, ChunkPlan p) {
+  __shared__ double tot[W][R * R + R];
   const long long b = blockIdx.x;
-  const int l = threadIdx.x;
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
   const long long NC = p.NC;
   if (b >= a.B) return;
   const double *bw = (const double *)(a.ws + p.bwd_off);
-  const long long q = (NC + 63) / 64;
-  const long long c0 = min(NC, (long long)l * q), c1 = min(NC, c0 + q);
-  Affine<R> F;
-  F.set_identity();
-  for (long long c = c1 - 1; c >= c0; --c) {
+  const long long q = (NC + 64 * W - 1) / (64 * W);
+  const long long c0 = min(NC, (long long)tid * q), c1 = min(NC, c0 + q);
+  auto load_map = [&](const double *sp) {
     Affine<R> f;
-    const double *sp = bw + (b * NC + c) * (R * R + R);
 #pragma unroll
     for (int i = 0; i < R; ++i) {
       f.g[i] = sp[R * R + i];
 #pragma unroll
       for (int j = 0; j < R; ++j) f.G[i][j] = sp[i * R + j];
     }
-    F = f.after(F);
-  }
+    return f;
+  };
+  Affine<R> F;
+  F.set_identity();
+  for (long long c = c1 - 1; c >= c0; --c) F = load_map(bw + (b * NC + c) * (R * R + R)).after(F);
 #pragma unroll
   for (int k = 1; k < 64; k <<= 1) {
     const Affine<R> o = F.shfl_down(k);
     if (l + k < 64) F = F.after(o);
   }
   if (l == 0) {
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      tot[w][R * R + i] = F.g[i];
+#pragma unroll
+      for (int j = 0; j < R; ++j) tot[w][i * R + j] = F.G[i][j];
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    for (int v = 1; v < W; ++v) F = F.after(load_map(tot[v]));
     double *o = a.seg_out + b * (R * R + R);
 #pragma unroll
     for (int i = 0; i < R; ++i) {
@@ -1382,7 +1410,16 @@ int launch_shape(const SmoothArgs &a, int algo, long long L) {
       if (rc) return rc;
       if (ph == 1) {  // the segment's aggregate element
         prof_mark(a.stream, "k_seg_elems");
-        hipLaunchKernelGGL((k_seg_elems<R>), dim3((unsigned)a.B), dim3(64), 0, a.stream, a, p);
+        const int sw1 = scan_waves(p.NC);
+        if (sw1 == 8)
+          hipLaunchKernelGGL((k_seg_elems<R, 8>), dim3((unsigned)a.B), dim3(512), 0, a.stream, a,
+                             p);
+        else if (sw1 == 4)
+          hipLaunchKernelGGL((k_seg_elems<R, 4>), dim3((unsigned)a.B), dim3(256), 0, a.stream, a,
+                             p);
+        else
+          hipLaunchKernelGGL((k_seg_elems<R, 1>), dim3((unsigned)a.B), dim3(64), 0, a.stream, a,
+                             p);
         prof_call_end(a.stream);
         return check_launch("k_seg_elems");
       }
@@ -1409,9 +1446,17 @@ int launch_shape(const SmoothArgs &a, int algo, long long L) {
       hipLaunchKernelGGL((k_c3_rerun<R, N, YT, AI, CI, LS, U>), dim3(gch), dim3(kBlock), 0,
                          a.stream, a, p);
       if ((rc = check_launch("k_c3_rerun"))) return rc;
-      if (ph == 2) {  // the segment's aggregate RTS map
+      if (ph == 2 && p.smooth) {  // the segment's aggregate RTS map
         prof_mark(a.stream, "k_seg_maps");
-        hipLaunchKernelGGL((k_seg_maps<R>), dim3((unsigned)a.B), dim3(64), 0, a.stream, a, p);
+        if (sw == 8)
+          hipLaunchKernelGGL((k_seg_maps<R, 8>), dim3((unsigned)a.B), dim3(512), 0, a.stream, a,
+                             p);
+        else if (sw == 4)
+          hipLaunchKernelGGL((k_seg_maps<R, 4>), dim3((unsigned)a.B), dim3(256), 0, a.stream, a,
+                             p);
+        else
+          hipLaunchKernelGGL((k_seg_maps<R, 1>), dim3((unsigned)a.B), dim3(64), 0, a.stream, a,
+                             p);
         prof_call_end(a.stream);
         return check_launch("k_seg_maps");
       }

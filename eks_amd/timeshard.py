@@ -42,7 +42,8 @@ class Segment:
     eks_smooth_seg phases on the current stream."""
 
     def __init__(self, obs, params, *, n: int, r: int, t_base: int, T_total: int,
-                 mode: str = "median", flags: int = 0, out=None, slot: str = "seg0"):
+                 mode: str = "median", flags: int = 0, out=None, slot: str = "seg0",
+                 want_out: bool = True, want_ms: bool = False):
         torch = _lib.require_gpu()
         if isinstance(obs, batch.Yev):
             B, T, E, nn = obs.shape
@@ -72,9 +73,11 @@ class Segment:
         self.B, self.T, self.E, self.n, self.r = B, T, E, n, r
         self.t_base, self.T_total, self.flags = t_base, T_total, flags
         self.mode = _lib.EKS_MEDIAN if mode == "median" else _lib.EKS_MEAN
-        if out is None:
+        if want_out and out is None:
             out = torch.empty((T, B, n), dtype=torch.float64, device=dev).permute(1, 0, 2)
-        self.out = out
+        self.out = out if want_out else None  # None: filter only (NLL), phases 1-2
+        self.ms = (torch.empty((B, T, r), dtype=torch.float64, device=dev)
+                   if want_ms and want_out else None)
         self.nll = torch.empty((B,), dtype=torch.float64, device=dev)
         self.status = torch.empty((B,), dtype=torch.int32, device=dev)
         lib = _lib.load()
@@ -93,13 +96,14 @@ class Segment:
         return self.t_base + self.T == self.T_total
 
     def phase(self, k: int, seg_in=None, stream=None) -> None:
-        seg_out = {1: self.elem, 2: self.map, 3: None}[k]
-        ob, ot, oj = self.out.stride()
+        seg_out = {1: self.elem, 2: self.map if self.out is not None else None, 3: None}[k]
+        ob, ot, oj = self.out.stride() if self.out is not None else (0, 0, 0)
         sb, st, se, sj = self.strides
         _lib.check(_lib.load().eks_smooth_seg(
             self.ptr, self.dt, self.B, self.T, self.E, self.n, self.r, sb, st, se, sj,
-            self.mode, self.params.data_ptr(), self.out.data_ptr(), ob, ot, oj,
-            self.nll.data_ptr(), self.ws.data_ptr(), self.ws.numel(), self.flags,
+            self.mode, self.params.data_ptr(),
+            self.out.data_ptr() if self.out is not None else None, ob, ot, oj,
+            self.ms.data_ptr() if self.ms is not None else None, self.nll.data_ptr(), self.ws.data_ptr(), self.ws.numel(), self.flags,
             self.status.data_ptr(), self.t_base, self.T_total, k,
             seg_in.data_ptr() if seg_in is not None else None,
             seg_out.data_ptr() if seg_out is not None else None, _lib.stream_ptr(stream)),
@@ -129,19 +133,24 @@ def split_frames(T_total: int, nseg: int, k: int) -> tuple[int, int]:
 
 
 def smooth_segments(obs, params, *, n: int, r: int, nseg: int, mode: str = "median",
-                    flags: int = 0, out=None):
+                    flags: int = 0, out=None, want_out: bool = True, want_ms: bool = False):
     """All nseg segments of the time-sharded path in one process (one GPU):
     the same three phases and two combines, with torch.stack standing in for
-    the all_gather.  Returns dict(out (B, T, n), nll (B,), status (B,))."""
+    the all_gather.  Returns dict(out (B, T, n) or None, ms (B, T, r) or None,
+    nll (B,), status (B,)); want_out=False is the filter-only NLL (phases 1-2)."""
     torch = _lib.require_gpu()
     B, T = obs.shape[0], obs.shape[1]
-    if out is None:
+    if not want_out:
+        out = None
+    elif out is None:
         out = torch.empty((T, B, n), dtype=torch.float64, device=obs.device).permute(1, 0, 2)
     segs = []
     for k in range(nseg):
         t0, tk = split_frames(T, nseg, k)
         segs.append(Segment(obs[:, t0:t0 + tk], params, n=n, r=r, t_base=t0, T_total=T,
-                            mode=mode, flags=flags, out=out[:, t0:t0 + tk], slot=f"seg{k}"))
+                            mode=mode, flags=flags, slot=f"seg{k}", want_out=want_out,
+                            want_ms=want_ms,
+                            out=out[:, t0:t0 + tk] if want_out else None))
     for s in segs:
         s.phase(1)
     elems = torch.stack([s.elem for s in segs])
@@ -149,15 +158,23 @@ def smooth_segments(obs, params, *, n: int, r: int, nseg: int, mode: str = "medi
         if k:
             combine(0, elems, nseg, k, r, s.state, s.status)
         s.phase(2, s.state if k else None)
+    if want_out:
+        _backward(segs, r)
+    status = segs[0].status.clone()
+    for s in segs[1:]:
+        status |= s.status
+    ms = torch.cat([s.ms for s in segs], dim=1) if want_ms and want_out else None
+    return dict(out=out, ms=ms, nll=sum(s.nll for s in segs), status=status)
+
+
+def _backward(segs, r):
+    import torch
+    nseg = len(segs)
     maps = torch.stack([s.map for s in segs])
     for k, s in enumerate(segs):
         if k < nseg - 1:
             combine(1, maps, nseg, k, r, s.mean, s.status)
         s.phase(3, s.mean if k < nseg - 1 else None)
-    status = segs[0].status.clone()
-    for s in segs[1:]:
-        status |= s.status
-    return dict(out=out, nll=sum(s.nll for s in segs), status=status)
 
 
 def _all_gather(x, group):
@@ -165,6 +182,8 @@ def _all_gather(x, group):
     HBM; gloo (the CPU test backend) goes through a host copy."""
     import torch
     import torch.distributed as dist
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return x.unsqueeze(0).contiguous()
     world = dist.get_world_size(group)
     if dist.get_backend(group) == "nccl":
         g = torch.empty((world,) + tuple(x.shape), dtype=x.dtype, device=x.device)
@@ -177,18 +196,22 @@ def _all_gather(x, group):
 
 def smooth_time_sharded(obs, params, *, n: int, r: int, t_base: int, T_total: int,
                         mode: str = "median", flags: int = 0, group=None, out=None,
-                        want_nll: bool = False):
+                        want_nll: bool = False, want_out: bool = True,
+                        want_ms: bool = False):
     """This rank's segment of a time-sharded smooth: obs (B, T, E, n) holds
     frames [t_base, t_base + T) of every trajectory; segments are ordered by
     rank (rank k holds segment k) and together cover [0, T_total).
 
-    Returns dict(out (B, T, n) of this segment, status (B,) this segment's
-    flags, nll (B,) summed over all segments if want_nll)."""
+    Returns dict(out (B, T, n) and ms (B, T, r) (if want_ms) of this
+    segment, status (B,) this segment's
+    flags, nll (B,) summed over all segments if want_nll); want_out=False is
+    the filter-only NLL (phases 1-2, one exchange + the NLL sum)."""
     import torch.distributed as dist
-    world = dist.get_world_size(group)
-    rank = dist.get_rank(group)
+    single = not dist.is_initialized()  # one process: a single segment, no exchange
+    world = 1 if single else dist.get_world_size(group)
+    rank = 0 if single else dist.get_rank(group)
     seg = Segment(obs, params, n=n, r=r, t_base=t_base, T_total=T_total, mode=mode,
-                  flags=flags, out=out, slot="seg")
+                  flags=flags, out=out, slot="seg", want_out=want_out, want_ms=want_ms)
     if (rank == 0) != seg.first or (rank == world - 1) != seg.last:
         raise ValueError(f"rank {rank} of {world} holds frames [{t_base}, {t_base + seg.T}) "
                          f"of {T_total}: segments must be ordered by rank")
@@ -197,11 +220,12 @@ def smooth_time_sharded(obs, params, *, n: int, r: int, t_base: int, T_total: in
     if rank:
         combine(0, elems, world, rank, r, seg.state, seg.status)
     seg.phase(2, seg.state if rank else None)
-    maps = _all_gather(seg.map, group)
-    if rank < world - 1:
-        combine(1, maps, world, rank, r, seg.mean, seg.status)
-    seg.phase(3, seg.mean if rank < world - 1 else None)
+    if want_out:
+        maps = _all_gather(seg.map, group)
+        if rank < world - 1:
+            combine(1, maps, world, rank, r, seg.mean, seg.status)
+        seg.phase(3, seg.mean if rank < world - 1 else None)
     nll = None
-    if want_nll:
+    if want_nll or not want_out:
         nll = _all_gather(seg.nll[:, None], group).sum(0)[:, 0]
-    return dict(out=seg.out, status=seg.status, nll=nll)
+    return dict(out=seg.out, ms=seg.ms, status=seg.status, nll=nll)

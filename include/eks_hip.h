@@ -193,9 +193,11 @@ int64_t eks_smooth_chunk_len(int64_t B, int64_t T, int r);
  *   phase 2: seg_in = that state (NULL on segment 0); seg_out (B, R*R + R) <-
  *            the segment's aggregate smoothing map ms_in -> ms_first;
  *   -> all-gather the maps, eks_seg_combine(kind 1) -> mean (B, R)
+ *            (filter only: out = NULL, nll != NULL -> nll = the segment's share,
+ *            no map, no phase 3)
  *   phase 3: seg_in = the smoothed mean entering the next segment (NULL on
- *            the last); writes out (and nll = the segment's share, whose sum
- *            over segments is eks_smooth's nll).
+ *            the last); writes out, ms (B, T, r) if not NULL, and nll = the
+ *            segment's share, whose sum over segments is eks_smooth's nll.
  * The workspace (eks_smooth_seg_workspace_bytes) must survive phases 1..3.
  * Results equal eks_smooth's to rounding (different association order).
  */
@@ -203,8 +205,8 @@ size_t eks_smooth_seg_workspace_bytes(int64_t B, int64_t T, int n, int r);
 int eks_smooth_seg(const void *obs, int obs_dtype, int64_t B, int64_t T, int E, int n, int r,
                    int64_t sb, int64_t st, int64_t se, int64_t sj, int mode,
                    const double *params, double *out, int64_t ob, int64_t ot, int64_t oj,
-                   double *nll, void *workspace, size_t workspace_bytes, int model_flags,
-                   int32_t *status, int64_t t_base, int64_t T_total, int phase,
+                   double *ms, double *nll, void *workspace, size_t workspace_bytes,
+                   int model_flags, int32_t *status, int64_t t_base, int64_t T_total, int phase,
                    const double *seg_in, double *seg_out, void *stream);
 /* kind 0: in = nseg gathered elements (nseg, B, EL) -> out = state entering
  * segment `self`; kind 1: in = gathered maps (nseg, B, R*R+R) -> out = mean

@@ -77,13 +77,19 @@ def test_segments_match_one_piece(kind, B, T, nseg):
     from eks_amd import batch, timeshard
     st, params, flags, r, n = _problem(kind, B, T)
     d = batch.make_time_major(st, dtype=np.float32)
-    ref = batch.smooth(d, params, n=n, r=r, flags=flags, algo=1, want_nll=True, check=True)
-    seg = timeshard.smooth_segments(d, params, n=n, r=r, nseg=nseg, flags=flags)
+    ref = batch.smooth(d, params, n=n, r=r, flags=flags, algo=1, want_nll=True, want_ms=True,
+                       check=True)
+    seg = timeshard.smooth_segments(d, params, n=n, r=r, nseg=nseg, flags=flags, want_ms=True)
     assert int((seg["status"] != 0).sum()) == 0
     o1, o2 = ref["out"].cpu().numpy(), seg["out"].cpu().numpy()
     assert np.isfinite(o1).all() and np.isfinite(o2).all()
     assert np.abs(o1 - o2).max() < 1e-8
+    assert float((seg["ms"] - ref["ms"]).abs().max()) < 1e-8
     np.testing.assert_allclose(seg["nll"].cpu().numpy(), ref["nll"].cpu().numpy(), rtol=1e-10)
+    # filter only (phases 1-2): the NLL shares sum to eks_smooth's filter-only NLL
+    fo = timeshard.smooth_segments(d, params, n=n, r=r, nseg=nseg, flags=flags, want_out=False)
+    assert fo["out"] is None
+    np.testing.assert_allclose(fo["nll"].cpu().numpy(), ref["nll"].cpu().numpy(), rtol=1e-10)
 
 
 @pytest.mark.gpu
@@ -128,6 +134,9 @@ def _worker(rank, world, port, q):
         ref = batch.smooth(full, params, n=n, r=r, flags=flags, algo=1, want_nll=True)
         err = float((res["out"] - ref["out"][:, t0:t0 + tk]).abs().max())
         nerr = float(((res["nll"] - ref["nll"]) / ref["nll"]).abs().max())
+        fo = timeshard.smooth_time_sharded(d, params, n=n, r=r, t_base=t0, T_total=T,
+                                           flags=flags, want_out=False)
+        nerr = max(nerr, float(((fo["nll"] - ref["nll"]) / ref["nll"]).abs().max()))
         q.put((rank, err, nerr, int((res["status"] != 0).sum())))
         dist.barrier()
     finally:
