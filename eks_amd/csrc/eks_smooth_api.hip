@@ -8,13 +8,21 @@ using namespace eks;
 
 namespace {
 
-// automatic choice: the time-parallel scan whenever it creates more than one
-// chunk per trajectory (i.e. B alone does not fill the GPU), else sequential
-// (and a requested time-parallel run with a single chunk runs sequentially)
-int pick_algo(long long B, long long T, int r, int algo) {
+// automatic choice: the sequential algorithm when one chunk covers the
+// trajectory (B alone fills the GPU); the two-pass algorithm 3 for the
+// (r, n) = (2, 2) single-view shape with many trajectories (whole 256-lane
+// blocks per chunk) and compile-time member counts; else the three-pass
+// time-parallel scan.  A requested time-parallel run with a single chunk
+// runs sequentially.
+int pick_algo(long long B, long long T, int n, int r, int E, int algo) {
   const long long L = chunk_len(B, T, r);
   if (algo == 1) return 1;
-  return L >= T ? 1 : 2;
+  if (L >= T) return 1;
+  const bool a3_ok = (E >= 3 && E <= 5) && T >= 2 * fine_len3(r, n);
+  if (algo == 3) return a3_ok ? 3 : 2;
+  if (algo == 2) return 2;
+  const bool many = uniform_lanes(B) && B >= 2048;
+  return (a3_ok && many && r == 2 && n == 2) ? 3 : 2;
 }
 
 bool shape_supported(int r, int n) {
@@ -34,9 +42,11 @@ int64_t eks_smooth_chunk_len(int64_t B, int64_t T, int r) {
 size_t eks_smooth_workspace_bytes(int64_t B, int64_t T, int n, int r, int E, int algo) {
   (void)E;
   if (B <= 0 || T <= 0 || r < 1 || n < 1) return 0;
-  const int al = pick_algo(B, T, r, algo);
+  const int al = pick_algo(B, T, n, r, E, algo);
   if (al == 1) return seq_workspace_bytes(B, T, r);
-  return make_plan(B, T, r, n, chunk_len(B, T, r)).total;
+  const size_t p2 = make_plan(B, T, r, n, chunk_len(B, T, r)).total;
+  // algo 3 smooths only: a filter-only (NLL) call of the same shape runs algo 2
+  return al == 3 ? std::max(p2, make_plan3(B, T, r, n).total) : p2;
 }
 
 // shared validation and dispatch of eks_smooth / eks_smooth_seg
@@ -56,18 +66,19 @@ static int smooth_call(const void *obs, int obs_dtype, int64_t B, int64_t T, int
   if (obs_dtype != EKS_F32 && obs_dtype != EKS_F64 && obs_dtype != EKS_YEV32 &&
       obs_dtype != EKS_YEV64)
     return set_err(EKS_ERR_ARG, "bad dtype");
-  if (algo < 0 || algo > 2) return set_err(EKS_ERR_ARG, "eks_smooth: algo %d unknown", algo);
+  if (algo < 0 || algo > 3) return set_err(EKS_ERR_ARG, "eks_smooth: algo %d unknown", algo);
   if (!shape_supported(r, n))
     return set_err(EKS_ERR_UNSUPPORTED,
                    "eks_smooth: (r=%d, n=%d) not compiled in (have (2,2) (3,4) (3,6) (3,8))", r, n);
   if ((model_flags & EKS_MODEL_C_IDENTITY) && r != n)
     return set_err(EKS_ERR_ARG, "eks_smooth: C = I needs r == n");
   if (B == 0) return EKS_OK;
-  const int al = phase ? 2 : pick_algo(B, T, r, algo);
+  int al = phase ? 2 : pick_algo(B, T, n, r, E, algo);
   const size_t need = phase ? make_plan(B, T, r, n, chunk_len(B, T, r)).total
                             : eks_smooth_workspace_bytes(B, T, n, r, E, al);
   if (!workspace || workspace_bytes < need)
     return set_err(EKS_ERR_ARG, "eks_smooth: workspace of %zu bytes needed", need);
+  if (al == 3 && !out) al = 2;  // filter only: algo 3 has no NLL-only mode
   hipStream_t s = (hipStream_t)stream;
   if (phase <= 1 && hipMemsetAsync(status, 0, (size_t)B * sizeof(int32_t), s) != hipSuccess)
     return set_err(EKS_ERR_HIP, "eks_smooth: hipMemsetAsync(status) failed");

@@ -575,6 +575,95 @@ EKS_DEV bool compose_state(double (&m)[R], double (&P)[R][R], const Elem<R> &E) 
   return ok;
 }
 
+// compose_state plus the chunk-level RTS map across the chunk.  With the
+// filtered (m, P) at the boundary x_b = x_{s-1} and the element of [s, e):
+//   p(x_b | y_{..e-1}) = N(mt, Pt),  Pt = (I + P Jb)^-1 P,  mt = (I + P Jb)^-1 (m + P eta)
+//   p(x_e | x_b, y_{s..e-1}) = N(Ab x_b + bb, Cb)   (x_e = x_{e-1})
+// so (x_b, x_e) is jointly Gaussian given y_{..e-1}, x_e's marginal is the
+// filtered state at e-1 (= compose_state), and since x_b is independent of
+// the later observations given x_e, the smoothed means obey
+//   ms_b = mt + G (ms_e - m'),   G = Pt Ab^T P'^-1
+// i.e. the affine map ms_b = G ms_e + g with g = mt - G m'.  This replaces
+// the per-step RTS recursion (eks/ensemble_kalman.py:158-161) composed over
+// the chunk; it needs P' (a filtered covariance) invertible, which fails
+// only for an exactly observed state (R_ii = 0) at the chunk's last step.
+// (m, P) are replaced by the filtered state at e-1.  false if singular.
+template <int R>
+EKS_DEV bool compose_state_rts(double (&m)[R], double (&P)[R][R], const Elem<R> &E,
+                               double (&G)[R][R], double (&g)[R]) {
+  double W[R][R], Mi[R][R], v[R], PAt[R][R];
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    double pe = m[i];
+#pragma unroll
+    for (int k = 0; k < R; ++k) pe = fma(P[i][k], E.eta[k], pe);
+    v[i] = pe;
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      double t = (i == j) ? 1.0 : 0.0, u = 0.0;
+#pragma unroll
+      for (int k = 0; k < R; ++k) {
+        t = fma(P[i][k], E.Jb[k][j], t);
+        u = fma(P[i][k], E.Ab[j][k], u);
+      }
+      W[i][j] = t;
+      PAt[i][j] = u;
+    }
+  }
+  bool ok = small_inverse<R>(W, Mi);  // (I + P Jb)^-1
+  double mt[R], XP[R][R];              // XP = Pt Ab^T
+  matvec<R, R>(Mi, v, mt);
+  matmul<R, R, R>(Mi, PAt, XP);
+  double mn[R], Pn[R][R];
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    double s = E.bb[i];
+#pragma unroll
+    for (int k = 0; k < R; ++k) s = fma(E.Ab[i][k], mt[k], s);
+    mn[i] = s;
+  }
+#pragma unroll
+  for (int i = 0; i < R; ++i)
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      double s = E.Cb[i][j];
+#pragma unroll
+      for (int k = 0; k < R; ++k) s = fma(E.Ab[i][k], XP[k][j], s);
+      Pn[i][j] = s;
+    }
+#pragma unroll
+  for (int i = 0; i < R; ++i)
+#pragma unroll
+    for (int j = 0; j < R; ++j) P[i][j] = 0.5 * (Pn[i][j] + Pn[j][i]);
+  double Pi[R][R];
+  ok = small_inverse<R>(P, Pi) && ok;
+  // an exactly observed coordinate leaves P' singular up to rounding: then
+  // det P' / prod diag P' (1 for a diagonal P', 0 for a singular one) is at
+  // rounding level and G would be noise -> report it (caller falls back)
+  {
+    double dg = 1.0, tr = 0.0;
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      dg *= P[i][i];
+      double s = 0.0;
+#pragma unroll
+      for (int k = 0; k < R; ++k) s = fma(P[i][k], Pi[k][i], s);
+      tr += s;  // trace(P' P'^-1) = R when the inverse is accurate
+    }
+    ok = ok && dg > 0.0 && fabs(tr - (double)R) < 1e-6;
+  }
+  matmul<R, R, R>(XP, Pi, G);
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    double s = mt[i];
+#pragma unroll
+    for (int k = 0; k < R; ++k) s = fma(-G[i][k], mn[k], s);
+    g[i] = s;
+    m[i] = mn[i];
+  }
+  return ok;
+}
+
 }  // namespace eks
 
 namespace eks {

@@ -1340,8 +1340,11 @@ int dispatch_members_c(int E, F &&f) {
   }
 }
 
+#include "two_pass.hpp"
+
 template <int R, int N, bool AI, bool CI>
 int launch_shape(const SmoothArgs &a, int algo, long long L) {
+  if (algo == 3) return launch_algo3<R, N, AI, CI>(a);
   const bool f32 = a.dtype == EKS_F32;
   const bool yev = a.dtype == EKS_YEV32 || a.dtype == EKS_YEV64;
   if (algo == 1) {

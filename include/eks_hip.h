@@ -164,7 +164,10 @@ int64_t eks_param_len(int n, int r);
  *   workspace / workspace_bytes: device scratch of at least
  *            eks_smooth_workspace_bytes(...) bytes (not zeroed by caller).
  *   algo     0 = automatic, 1 = sequential (one lane per trajectory),
- *            2 = time-parallel chunked scan
+ *            2 = time-parallel chunked scan, three passes,
+ *            3 = time-parallel, two passes over the members (chunk-level RTS
+ *            maps; smoothing only: a filter-only call runs algo 2; needs
+ *            E in 3..5 or y / ev planes, else algo 2)
  *   status   (B) int32, REQUIRED; zeroed by the call, then bit flags as above.
  */
 size_t eks_smooth_workspace_bytes(int64_t B, int64_t T, int n, int r, int E, int algo);

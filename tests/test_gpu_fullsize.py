@@ -2,8 +2,9 @@
 x 5 members x 10 000 frames, 1.74e8 keypoint-timesteps) through properties
 that do not need the CPU oracle (which would take hours at this size):
 
-* the time-parallel algorithm (algo 2, 16 chunks per trajectory) equals the
-  sequential recursion (algo 1) on every trajectory (max|d| < 1e-8 px);
+* the time-parallel algorithms (algo 2, 16 chunks per trajectory; algo 3,
+  625 chunks of 16 frames) equal the sequential recursion (algo 1) on every
+  trajectory (max|d| < 1e-8 px);
 * translation equivariance: shifting every member by (dx, dy) shifts the
   model offsets and the smoothed outputs by exactly that (to rounding);
 * the device fit + hand-off path equals fit + smooth on the members.
@@ -39,6 +40,11 @@ def test_algo2_equals_sequential_full_size(work):
     a1 = batch.smooth(obs, params, n=2, r=2, algo=1, flags=flags, check=True)["out"]
     d = (a2 - a1).abs().max().item()
     assert d < 1e-8, d
+    del a2
+    r3 = batch.smooth(obs, params, n=2, r=2, algo=3, flags=flags)
+    assert (r3["status"] == 0).all()
+    d3 = (r3["out"] - a1).abs().max().item()
+    assert d3 < 1e-8, d3
 
 
 def test_translation_equivariance(work):

@@ -211,12 +211,13 @@ def _oracle_smooth_batch(stacks, models, O):
     return outs
 
 
-@pytest.mark.parametrize("algo", [1, 2])
+@pytest.mark.parametrize("algo", [1, 2, 3])
 @pytest.mark.parametrize("r,n,E", [(2, 2, 5), (3, 4, 5), (3, 6, 4), (3, 8, 5), (2, 2, 11),
                                    (2, 2, 3)])
 def test_fused_batch_vs_oracle(torch, r, n, E, algo):
-    """B independent trajectories with different models and layouts, both
-    algorithms (1 = sequential, 2 = time-parallel chunked scan)."""
+    """B independent trajectories with different models and layouts, every
+    algorithm (1 = sequential, 2 = time-parallel chunked scan, 3 = two-pass
+    time-parallel; E = 11 is not compiled for algo 3, which then runs 2)."""
     from eks_amd import batch, synthetic
     from oracle import eks_oracle as O
     rng = np.random.default_rng(100 * r + n)
@@ -310,6 +311,10 @@ def test_time_parallel_long_trajectories(torch, kind):
     n2 = r2["nll"].cpu().numpy()
     assert np.abs(o1 - o2).max() < 1e-8
     np.testing.assert_allclose(n2, n1, rtol=1e-10)
+    r3 = batch.smooth(d, params, n=n, r=r, algo=3, flags=flags, want_nll=True)
+    assert (r3["status"] == 0).all()
+    assert np.abs(r3["out"].cpu().numpy() - o1).max() < 1e-8
+    np.testing.assert_allclose(r3["nll"].cpu().numpy(), n1, rtol=1e-10)
     ref = _oracle_smooth_batch([st[0], st[B - 1]], [models[0], models[B - 1]], O)
     assert np.abs(o2[0] - ref[0]).max() < OUT_TOL
     assert np.abs(o2[B - 1] - ref[1]).max() < OUT_TOL
@@ -342,13 +347,13 @@ def test_fused_edge_cases(torch):
                  Q=np.array([[0.5, 0.1], [0.1, 0.4]]), C=np.eye(2), offset=np.array([100., 100.]))
         params = batch.pack_params(m["m0"], m["S0"], m["A"], m["Q"], m["C"], m["offset"])
         ref = _oracle_smooth_batch([st[0]], [m], O)[0]
-        for algo in (1, 2):
-            res = batch.smooth(batch.make_time_major(st), params, n=2, r=2, algo=algo)
+        for algo in (1, 2, 3):
+            res = batch.smooth(batch.make_time_major(st), params, n=2, r=2, algo=algo, check=True)
             assert np.abs(res["out"][0].cpu().numpy() - ref).max() < OUT_TOL, (T, algo)
     st = rng.normal(100, 5, size=(1, 5, 50, 2))
     st[0, 2, 20, 1] = np.nan
     ref = _oracle_smooth_batch([st[0]], [m], O)[0]
-    for algo in (1, 2):
+    for algo in (1, 2, 3):
         res = batch.smooth(batch.make_time_major(st), params, n=2, r=2, algo=algo)
         out = res["out"][0].cpu().numpy()
         np.testing.assert_array_equal(np.isnan(out), np.isnan(ref))
@@ -668,6 +673,7 @@ def test_torch_ops_match_batch_api(torch):
 # fit -> smooth ensemble hand-off (EKS_YEV32 / EKS_YEV64): bit-identical
 @pytest.mark.parametrize("kind,V,E,dtype,mode,algo", [
     ("singleview", 1, 5, "f32", "median", 0), ("singleview", 1, 5, "f32", "median", 1),
+    ("singleview", 1, 5, "f32", "median", 3), ("singleview", 1, 4, "f64", "mean", 3),
     ("singleview", 1, 4, "f64", "median", 2), ("singleview", 1, 3, "f32", "mean", 0),
     ("multicam", 4, 5, "f32", "median", 0), ("multicam", 2, 3, "f64", "median", 1)])
 def test_fit_yev_handoff_bit_exact(torch, kind, V, E, dtype, mode, algo):
