@@ -213,8 +213,9 @@ def workload_singleview(torch, a, dev, rank, world, config):
                 cfg=dict(videos=a.videos if config == 4 else 1, keypoints=K, members=E, frames=T,
                          trajectories_per_rank=B, smooth_param=a.smooth_param,
                          quantile_keep=a.quantile_keep),
+                shape=(B, T, 2, 2, E),
                 key=f"config{config}-singleview-v{len(videos) * world if config == 4 else 1}"
-                    f"-k{K}-e{E}-t{T}-n{world}-{a.scaling}-a{a.algo}",
+                    f"-k{K}-e{E}-t{T}-n{world}-{a.scaling}",
                 out=out, videos=videos)
 
 
@@ -264,7 +265,7 @@ def workload_multiview(torch, a, dev, rank, world):
                 units=K * T, bytes_per_unit=E * n * 4 + n * 8, cpu=cpu, cpu_default=5, desc=desc,
                 cfg=dict(cameras=V, keypoints=K, members=E, frames=T,
                          smooth_param=a.smooth_param, quantile_keep=a.quantile_keep),
-                key=f"config3-multiview-k{K}-e{E}-t{T}-n{world}-a{a.algo}")
+                shape=(K, T, n, 3, E), key=f"config3-multiview-k{K}-e{E}-t{T}-n{world}")
 
 
 def workload_pupil(torch, a, dev, rank, world):
@@ -343,7 +344,8 @@ def workload_pupil(torch, a, dev, rank, world):
                 bytes_per_unit=(32 * E + 88) / 4, cpu=cpu, cpu_default=1, desc=desc,
                 timeshard=a.timeshard,
                 cfg=dict(frames=T, keypoints=4, members=E, candidates=len(cands)),
-                key=f"config5-pupil-t{T}-n{world}-a{a.algo}{'-ts' if a.timeshard else ''}",
+                shape=(1, T, 8, 3, E),
+                key=f"config5-pupil-t{T}-n{world}{'-ts' if a.timeshard else ''}",
                 extra=lambda: dict(
                     sweep_candidates=len(cands),
                     best_model=[float(x) for x in np.diag(cands[int(state['best'])]['A'])]))
@@ -382,6 +384,9 @@ def main():
     torch.cuda.synchronize()
     setup_s = time.perf_counter() - t_setup
     step = w["step"]
+    # the algorithm eks_smooth resolves for this shape (0 = automatic choice)
+    algo_used = int(_lib.load().eks_smooth_algo(*w["shape"], a.algo))
+    w["key"] += f"-a{algo_used}"
 
     for _ in range(a.warmup):
         step()
@@ -502,7 +507,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic",
-            "config": dict(workload=w["desc"], algo=a.algo, parallelism=par, **w["cfg"]),
+            "config": dict(workload=w["desc"], algo=algo_used, parallelism=par, **w["cfg"]),
             "roofline": {
                 "bound": "hbm",
                 "achieved": achieved,

@@ -47,6 +47,7 @@ SIGNATURES = {
     "eks_smooth": (_i32, [_p, _i32, _i64, _i64, _i32, _i32, _i32, _i64, _i64, _i64, _i64, _i32,
                           _p, _p, _i64, _i64, _i64, _p, _p, _p, _sz, _i32, _i32, _p, _p]),
     "eks_smooth_chunk_len": (_i64, [_i64, _i64, _i32]),
+    "eks_smooth_algo": (_i32, [_i64, _i64, _i32, _i32, _i32, _i32]),
     "eks_smooth_seg_workspace_bytes": (_sz, [_i64, _i64, _i32, _i32]),
     "eks_smooth_seg": (_i32, [_p, _i32, _i64, _i64, _i32, _i32, _i32, _i64, _i64, _i64, _i64,
                               _i32, _p, _p, _i64, _i64, _i64, _p, _p, _p, _sz, _i32, _p, _i64,

@@ -39,6 +39,11 @@ int64_t eks_smooth_chunk_len(int64_t B, int64_t T, int r) {
   return L >= T ? 0 : L;
 }
 
+int eks_smooth_algo(int64_t B, int64_t T, int n, int r, int E, int algo) {
+  if (B <= 0 || T <= 0 || r < 1 || n < 1 || algo < 0 || algo > 3) return 0;
+  return pick_algo(B, T, n, r, E, algo);
+}
+
 size_t eks_smooth_workspace_bytes(int64_t B, int64_t T, int n, int r, int E, int algo) {
   (void)E;
   if (B <= 0 || T <= 0 || r < 1 || n < 1) return 0;

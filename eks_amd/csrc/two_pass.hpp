@@ -48,6 +48,9 @@ constexpr int kNF = EKS_K3_NF;  // fine chunks per coarse chunk (waves of a k3_e
 #define EKS_K3_DF 2      // member prefetch distance (steps) of k3_final
 #endif
 constexpr int kNS = 2;   // sub-chunks per fine chunk in k3_final
+#ifndef EKS_K3_FINAL
+#define EKS_K3_FINAL k3_final_s  // state-stash final pass (k3_final: (y, ev) stash + re-run)
+#endif
 
 constexpr int sub_len3(int r, int n) { return sub_len_c(r, n); }
 constexpr int fine_len3(int r, int n) { return kNS * sub_len3(r, n); }
@@ -673,6 +676,162 @@ __global__ __launch_bounds__(kBlock) void k3_final(SmoothArgs a, Plan3 p) {
   if (!ok) flag(a.status, b, EKS_STATUS_SINGULAR);
 }
 
+// P4, state-stash form: the forward sweep keeps the FILTERED STATE of every
+// step (LDS for the early sub-chunks, registers for the last one) instead of
+// (y, ev), so the backward sweep computes the RTS gains without re-running
+// the filter (one filter pass per step instead of 1.5).
+template <int R, int N, int E, typename T, typename YT, bool AI, bool CI, int LS>
+__global__ __launch_bounds__(kBlock) void k3_final_s(SmoothArgs a, Plan3 p) {
+  constexpr int KS = R + Sym<R>::len;
+  constexpr int D = EKS_K3_DF;
+  constexpr int NST = (kNS - 1) * LS;  // steps kept in LDS
+  __shared__ double fs[NST][KS][kBlock];
+  Lane<true> ln;
+  const long long B = a.B, TT = a.T;
+  if (!ln.init(B, p.NCf)) return;
+  const long long c = ln.c;
+  const unsigned b = ln.b;
+  const int tid = threadIdx.x;
+  Model<R, N> md;
+  md.load(a.params + (long long)b * ParamLayout<R, N>::len, c == 0);
+  const long long s = c * p.L, e = min(TT, s + p.L);
+  const bool last = e == TT;
+  const int nsub = (int)((e - s + LS - 1) / LS);
+  typename SrcOf<E, N, T, D>::type src;
+  src.init(a, b);
+#pragma unroll
+  for (int q = 0; q < D; ++q)
+    if (s + q < e) src.fetch(q, s + q);
+  double m[R], P[R][R];
+  if (c == 0) {
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      m[i] = md.m0[i];
+#pragma unroll
+      for (int j = 0; j < R; ++j) P[i][j] = md.S0[i][j];
+    }
+  } else {
+    load_state_pl<R>((const double *)(a.ws + p.fcs_off), c * KS, B, b, m, P);
+  }
+  double msE[R];
+#pragma unroll
+  for (int i = 0; i < R; ++i)
+    msE[i] = last ? 0.0 : pl((const double *)(a.ws + p.fms_off), c * R + i, B, b);
+  bool ok = true;
+  NllAcc acc;
+  double Mr[LS][KS];  // filtered states of the last sub-chunk
+  auto pack = [&](double (&dst)[KS]) {
+    int k = 0;
+#pragma unroll
+    for (int i = 0; i < R; ++i) dst[k++] = m[i];
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+#pragma unroll
+      for (int j = i; j < R; ++j) dst[k++] = P[i][j];
+  };
+#pragma unroll
+  for (int i = 0; i < kNS * LS; ++i) {
+    const long long t = s + i;
+    const int k = i / LS, q = i % LS;
+    if (t < e) {
+      double avg[N], rv[N], y[N];
+      src.get(i % D, avg, rv);
+      if (t + D < e) src.fetch(i % D, t + D);
+#pragma unroll
+      for (int j = 0; j < N; ++j) y[j] = avg[j] - md.off[j];
+      if (t > 0) kf_predict<R, AI>(m, P, md.A, md.Q);
+      kf_update<R, N, CI>(m, P, md.C, y, rv, acc, ok);
+      if (k == nsub - 1) {
+        pack(Mr[q]);
+      } else if (k < kNS - 1) {
+        double st[KS];
+        pack(st);
+#pragma unroll
+        for (int u = 0; u < KS; ++u) fs[i][u][tid] = st[u];
+      }
+    }
+  }
+  if (a.nll) pl((double *)(a.ws + p.nllp_off), c, B, b) = acc.value((double)(e - s) * N);
+  double *outb = a.out + (long long)b * a.ob;
+  const bool vec2 = N == 2 && a.oj == 1 && ((a.ob | a.ot) & 1) == 0 &&
+                    (((uintptr_t)a.out) & 15) == 0;
+  double ms[R];
+#pragma unroll
+  for (int i = 0; i < R; ++i) ms[i] = 0.0;
+  auto emit = [&](long long t) {
+    if constexpr (N == 2) {
+      if (vec2) {
+        double cm[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          if constexpr (CI) {
+            cm[j] = ms[j] + md.off[j];
+          } else {
+            double u = 0.0;
+#pragma unroll
+            for (int k = 0; k < R; ++k) u = fma(md.C[j][k], ms[k], u);
+            cm[j] = u + md.off[j];
+          }
+        }
+        *(double2 *)(outb + t * a.ot) = make_double2(cm[0], cm[1]);
+      } else {
+        project_store<R, N, CI>(outb + t * a.ot, a.oj, md.C, ms, md.off);
+      }
+    } else {
+      project_store<R, N, CI>(outb + t * a.ot, a.oj, md.C, ms, md.off);
+    }
+    if (a.ms) store_vec<R>(a.ms + ((long long)b * TT + t) * R, ms);
+  };
+  // one RTS step backwards from the filtered state st of step t
+  auto rts_step = [&](const double (&st)[KS]) {
+    double mf[R], Pf[R][R], J[R][R], d[R], nx[R];
+    int k = 0;
+#pragma unroll
+    for (int i = 0; i < R; ++i) mf[i] = st[k++];
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+#pragma unroll
+      for (int j = i; j < R; ++j) Pf[i][j] = Pf[j][i] = st[k++];
+    ok = rts_gain<R, AI>(mf, Pf, md.A, md.Q, J, d) && ok;
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      double sm = d[i];
+#pragma unroll
+      for (int u = 0; u < R; ++u) sm = fma(J[i][u], ms[u], sm);
+      nx[i] = sm;
+    }
+#pragma unroll
+    for (int i = 0; i < R; ++i) ms[i] = nx[i];
+  };
+  // the last sub-chunk, from registers; its last step's mean is known
+#pragma unroll
+  for (int q = LS - 1; q >= 0; --q) {
+    const long long t = s + (long long)(nsub - 1) * LS + q;
+    if (t < e) {
+      if (t == e - 1) {
+#pragma unroll
+        for (int i = 0; i < R; ++i) ms[i] = last ? Mr[q][i] : msE[i];
+      } else {
+        rts_step(Mr[q]);
+      }
+      emit(t);
+    }
+  }
+  // the earlier sub-chunks, from LDS
+  for (int k = nsub - 2; k >= 0; --k) {
+#pragma unroll
+    for (int q = LS - 1; q >= 0; --q) {
+      const int i = k * LS + q;
+      double st[KS];
+#pragma unroll
+      for (int u = 0; u < KS; ++u) st[u] = fs[i][u][tid];
+      rts_step(st);
+      emit(s + i);
+    }
+  }
+  if (!ok) flag(a.status, b, EKS_STATUS_SINGULAR);
+}
+
 // NLL of each trajectory = sum of its fine chunks' shares (fixed order)
 template <int R>
 __global__ __launch_bounds__(64) void k3_nll(SmoothArgs a, Plan3 p) {
@@ -715,7 +874,7 @@ int launch_algo3(const SmoothArgs &a) {
     hipLaunchKernelGGL((k3_fine<R>), dim3(g3), dim3(kBlock), 0, a.stream, a, p);
     if ((rc = check_launch("k3_fine"))) return rc;
     prof_mark(a.stream, "k3_final");
-    hipLaunchKernelGGL((k3_final<R, N, EE, Tp, YT, AI, CI, LS>), dim3(g4), dim3(kBlock), 0,
+    hipLaunchKernelGGL((EKS_K3_FINAL<R, N, EE, Tp, YT, AI, CI, LS>), dim3(g4), dim3(kBlock), 0,
                        a.stream, a, p);
     if ((rc = check_launch("k3_final"))) return rc;
     if (a.nll) {

@@ -181,6 +181,11 @@ int eks_smooth(const void *obs, int obs_dtype, int64_t B, int64_t T, int E, int 
  * would be chosen automatically).  Exposed for tests and DESIGN.md. */
 int64_t eks_smooth_chunk_len(int64_t B, int64_t T, int r);
 
+/* The algorithm (1, 2 or 3) an eks_smooth call with these arguments runs
+ * (smoothing calls; a filter-only call that resolves to 3 runs 2).  Exposed
+ * for the bench line and tests. */
+int eks_smooth_algo(int64_t B, int64_t T, int n, int r, int E, int algo);
+
 /*
  * Time-sharded smoothing (SURVEY.md §8(e) "shard the time axis"): the frames
  * of every trajectory are split into nseg contiguous segments, segment k on

@@ -29,6 +29,14 @@ def test_limits_and_sizes():
     L = lib.eks_smooth_chunk_len(17, 100000, 2)
     assert 16 <= L < 100000 and L % 8 == 0
     assert lib.eks_smooth_chunk_len(1 << 20, 1000, 2) == 0  # enough trajectories: sequential
+    # automatic algorithm: two-pass for many single-view trajectories, the
+    # three-pass scan for few or multi-view ones, sequential for very many
+    assert lib.eks_smooth_algo(17408, 10000, 2, 2, 5, 0) == 3
+    assert lib.eks_smooth_algo(17, 100000, 2, 2, 5, 0) == 2
+    assert lib.eks_smooth_algo(17408, 10000, 8, 3, 5, 0) == 2
+    assert lib.eks_smooth_algo(1 << 20, 1000, 2, 2, 5, 0) == 1
+    assert lib.eks_smooth_algo(17408, 10000, 2, 2, 11, 3) == 2  # E = 11: no algo-3 kernels
+    assert lib.eks_smooth_algo(4, 100, 2, 2, 5, 9) == 0
     assert lib.eks_smooth_workspace_bytes(17, 100000, 2, 2, 5, 2) >= 17 * 100000 * 2 * 16
 
 

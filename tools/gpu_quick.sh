@@ -7,7 +7,8 @@ if [ -n "$PYTEST_K" ]; then
   timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread -k "$PYTEST_K" > gpurun_out/q_pytest.log 2>&1
   rc=$?; echo "pytest rc=$rc"; tail -1 gpurun_out/q_pytest.log; [ $rc -eq 0 ] || exit $rc
 fi
-for args in ${BENCHES:-"--videos 1024" "--videos 128"}; do
+for nv in ${VIDEOS:-1024 128}; do
+  args="--videos $nv"
   tag=$(echo $args | tr -d ' -')
   timeout -k 10 300 python bench.py --steps 10 --warmup 2 --no-cpu-baseline $args > gpurun_out/q_$tag.log 2>&1 || exit $?
   python - gpurun_out/q_$tag.log "$args" <<'PY'

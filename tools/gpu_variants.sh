@@ -5,7 +5,8 @@ mkdir -p gpurun_out
 export PYTHONDONTWRITEBYTECODE=1
 for v in default ${VARIANTS:-$(ls exp)}; do
   if [ "$v" = default ]; then unset EKS_LIB; else export EKS_LIB=exp/$v/libeks_hip.so; fi
-  for args in ${BENCHES:-"--videos 1024" "--videos 128"}; do
+  for nv in ${VIDEOS:-1024 128}; do
+  args="--videos $nv"
     tag=$(echo $args | tr -d ' -')
     timeout -k 10 300 python bench.py --steps 10 --warmup 2 --no-cpu-baseline $args > gpurun_out/v_${v}_$tag.log 2>&1 || exit $?
     python - gpurun_out/v_${v}_$tag.log "$v $args" <<'PY'
