@@ -37,10 +37,14 @@
 // singular boundary covariance (exactly observed state at a chunk's last
 // step) sets EKS_STATUS_SCAN; batch.smooth(check=True) then re-runs algo 1.
 
-#ifndef EKS_K3_NF
-#define EKS_K3_NF 4
+#ifndef EKS_K3_FPL
+#define EKS_K3_FPL 1     // fine chunks per k3_elem lane (2: 128-step coarse chunks, halves k3_coarse but 256 VGPRs in k3_elem, measured slower)
 #endif
-constexpr int kNF = EKS_K3_NF;  // fine chunks per coarse chunk (waves of a k3_elem block)
+#ifndef EKS_K3_WV
+#define EKS_K3_WV 4      // waves per k3_elem block
+#endif
+constexpr int kFPL = EKS_K3_FPL, kWV = EKS_K3_WV;
+constexpr int kNF = kFPL * kWV;  // fine chunks per coarse chunk
 #ifndef EKS_K3_D
 #define EKS_K3_D 2       // member prefetch distance (steps) of k3_elem
 #endif
@@ -48,9 +52,34 @@ constexpr int kNF = EKS_K3_NF;  // fine chunks per coarse chunk (waves of a k3_e
 #define EKS_K3_DF 2      // member prefetch distance (steps) of k3_final
 #endif
 constexpr int kNS = 2;   // sub-chunks per fine chunk in k3_final
-#ifndef EKS_K3_FINAL
-#define EKS_K3_FINAL k3_final_s  // state-stash final pass (k3_final: (y, ev) stash + re-run)
+// occupancy target of the streaming kernels: their LDS / state already limit
+// them to 2 waves per SIMD, so the compiler may spend the whole register file
+// on keeping member prefetches in flight instead of trimming it for waves
+// that could never be resident
+#ifndef EKS_K3_FULLPATH
+#define EKS_K3_FULLPATH 0  // 1: guard-free unrolled step loop in k3_final_s (measured 35 % slower)
 #endif
+// Keep the member prefetches where they are issued: without a scheduling
+// barrier the machine scheduler sinks them next to their use (to save
+// registers), so every step waits for its own loads (vmcnt(0) each step).
+#ifndef EKS_PIN
+#define EKS_PIN 0  // measured neutral
+#endif
+#if EKS_PIN
+#define EKS_PIN_LOADS() __builtin_amdgcn_sched_barrier(0)
+#else
+#define EKS_PIN_LOADS() ((void)0)
+#endif
+#ifndef EKS_K3_WPE
+#define EKS_K3_WPE  // e.g. __attribute__((amdgpu_waves_per_eu(2, 2))): measured spills
+#endif
+#ifndef EKS_K3E_WPE
+#define EKS_K3E_WPE
+#endif
+#ifndef EKS_K3_MERGED
+#define EKS_K3_MERGED 0  // 1: the fine walk inside the final pass (measured slower: prologue latency)
+#endif
+
 
 constexpr int sub_len3(int r, int n) { return sub_len_c(r, n); }
 constexpr int fine_len3(int r, int n) { return kNS * sub_len3(r, n); }
@@ -78,8 +107,10 @@ inline Plan3 make_plan3(long long B, long long T, int r, int n) {
   p.ccs_off = take((size_t)p.NCc * state_len(r) * Bz * 8);
   p.cmap_off = take((size_t)p.NCc * (r * r + r) * Bz * 8);
   p.cms_off = take((size_t)(p.NCc + 1) * r * Bz * 8);
-  p.fcs_off = take((size_t)p.NCf * state_len(r) * Bz * 8);
-  p.fms_off = take((size_t)p.NCf * r * Bz * 8);
+  if (!EKS_K3_MERGED) {  // per-fine-chunk start states / last-step means (k3_fine)
+    p.fcs_off = take((size_t)p.NCf * state_len(r) * Bz * 8);
+    p.fms_off = take((size_t)p.NCf * r * Bz * 8);
+  }
   p.nllp_off = take((size_t)p.NCf * Bz * 8);
   p.total = off;
   return p;
@@ -166,18 +197,23 @@ EKS_DEV void load_elem_pl(const double *base, long long c, long long B, unsigned
 // P1: fine elements + coarse aggregates
 // ---------------------------------------------------------------------------
 template <int R, int N, int E, typename T, bool AI, bool CI>
-__global__ __launch_bounds__(64 * kNF) void k3_elem(SmoothArgs a, Plan3 p) {
+__global__ __launch_bounds__(64 * kWV) EKS_K3E_WPE void k3_elem(SmoothArgs a, Plan3 p) {
   constexpr int EL = Elem<R>::len;
   constexpr int D = EKS_K3_D;
-  __shared__ double sh[kNF][EL][64];
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __shared__ double sh[kWV][EL][64];
+  // the wave index is uniform: keep it (and every time index) in SGPRs
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63;
   const long long B = a.B, TT = a.T;
   const long long ng = (B + 63) / 64;
   const long long cc = blockIdx.x / ng;
   const unsigned b = (unsigned)((blockIdx.x - cc * ng) * 64 + l);
-  const long long f = cc * kNF + w;
-  const bool live = (long long)b < B && f < p.NCf;
   bool ok = true, okf = true;  // element / composition, and the plain filter of chunk 0
+  Elem<R> Acc;  // the lane's kFPL consecutive fine chunks, composed
+  Acc.set_identity();
+#pragma unroll 1
+  for (int u = 0; u < kFPL; ++u) {
+  const long long f = cc * kNF + w * kFPL + u;
+  const bool live = (long long)b < B && f < p.NCf;
   Elem<R> El;
   El.set_identity();
   if (live) {
@@ -187,23 +223,49 @@ __global__ __launch_bounds__(64 * kNF) void k3_elem(SmoothArgs a, Plan3 p) {
     const long long s = f * p.L, e = min(TT, s + p.L);
     typename SrcOf<E, N, T, D>::type src;
     src.init(a, b);
-#pragma unroll
-    for (int q = 0; q < D; ++q)
-      if (s + q < e) src.fetch(q, s + q);
     // the step loop, specialised per chunk kind (hoisted branch: the filter
-    // state and the element are never live together)
+    // state and the element are never live together).  Full chunks (all but
+    // a trajectory's last) run a compile-time loop whose prefetches are
+    // unconditional: a load under a lane-divergent `if` is merged into its
+    // ring slot by a copy that waits for it, i.e. no prefetch at all.
     auto stream = [&](auto &&absorb) {
-      for (long long t0 = s; t0 < e; t0 += D) {
+      constexpr int LF = fine_len3(R, N);
+      if (e - s == LF) {
+        // full chunk: the same loads on every path (see k3_final_s); the
+        // clamped tail re-reads the last step (a cache hit) instead of branching
 #pragma unroll
-        for (int q = 0; q < D; ++q) {
-          const long long t = t0 + q;
-          if (t < e) {
+        for (int q = 0; q < D; ++q) src.fetch(q, s + q);
+#pragma unroll 1
+        for (int i0 = 0; i0 < LF; i0 += D) {
+#pragma unroll
+          for (int q = 0; q < D; ++q) {
+            const long long t = s + i0 + q;
             double avg[N], rv[N], y[N];
             src.get(q, avg, rv);
-            if (t + D < e) src.fetch(q, t + D);
+            src.fetch(q, min(t + D, s + LF - 1));
+            EKS_PIN_LOADS();
 #pragma unroll
             for (int j = 0; j < N; ++j) y[j] = avg[j] - md.off[j];
             absorb(t, y, rv);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < D; ++q)
+          if (s + q < e) src.fetch(q, s + q);
+        for (long long t0 = s; t0 < e; t0 += D) {
+#pragma unroll
+          for (int q = 0; q < D; ++q) {
+            const long long t = t0 + q;
+            if (t < e) {
+              double avg[N], rv[N], y[N];
+              src.get(q, avg, rv);
+              if (t + D < e) src.fetch(q, t + D);
+              EKS_PIN_LOADS();
+#pragma unroll
+              for (int j = 0; j < N; ++j) y[j] = avg[j] - md.off[j];
+              absorb(t, y, rv);
+            }
           }
         }
       }
@@ -237,12 +299,20 @@ __global__ __launch_bounds__(64 * kNF) void k3_elem(SmoothArgs a, Plan3 p) {
       });
     }
     store_elem_pl<R>((double *)(a.ws + p.fel_off), f, B, b, El);
+    if (u == 0) {
+      Acc = El;
+    } else {
+      Elem<R> Et;
+      ok = compose_elem<R>(Acc, El, Et) && ok;
+      Acc = Et;
+    }
   }
-  // coarse element = ordered tree over the block's waves (log2 kNF rounds;
+  }
+  // coarse element = ordered tree over the block's waves (log2 kWV rounds;
   // dead waves hold the identity, which composes exactly)
-  El.store(&sh[w][0][l], 64);
+  Acc.store(&sh[w][0][l], 64);
 #pragma unroll
-  for (int st2 = 1; st2 < kNF; st2 <<= 1) {
+  for (int st2 = 1; st2 < kWV; st2 <<= 1) {
     __syncthreads();
     if ((w & (2 * st2 - 1)) == 0) {
       Elem<R> Ea, Eb, Et;
@@ -257,7 +327,8 @@ __global__ __launch_bounds__(64 * kNF) void k3_elem(SmoothArgs a, Plan3 p) {
     Ec.load(&sh[0][0][l], 64);
     store_elem_pl<R>((double *)(a.ws + p.cel_off), cc, B, b, Ec);
   }
-  if (live) flag(a.status, b, (ok ? 0 : EKS_STATUS_SCAN) | (okf ? 0 : EKS_STATUS_SINGULAR));
+  if ((long long)b < B)
+    flag(a.status, b, (ok ? 0 : EKS_STATUS_SCAN) | (okf ? 0 : EKS_STATUS_SINGULAR));
 }
 
 // ---------------------------------------------------------------------------
@@ -303,7 +374,11 @@ __global__ __launch_bounds__(64 * kNP) void k3_coarse(SmoothArgs a, Plan3 p) {
 #pragma unroll
   for (int u = 0; u < kPF; ++u)
     if (c0 + u < c1) load_elem_pl<R>(cel, c0 + u, B, b, ring[u]);
+#ifdef EKS_K3C_SKIP_A  // timing experiment only
+  for (long long c = c0; c < c0; c += kPF) {
+#else
   for (long long c = c0; c < c1; c += kPF) {
+#endif
 #pragma unroll
     for (int u = 0; u < kPF; ++u) {
       if (c + u < c1) {
@@ -352,7 +427,11 @@ __global__ __launch_bounds__(64 * kNP) void k3_coarse(SmoothArgs a, Plan3 p) {
 #pragma unroll
   for (int u = 0; u < kPF; ++u)
     if (c + u < c1) load_elem_pl<R>(cel, c + u, B, b, ring[u]);
+#ifdef EKS_K3C_SKIP_C  // timing experiment only
+  for (; c < c0; c += kPF) {
+#else
   for (; c < c1; c += kPF) {
+#endif
 #pragma unroll
     for (int u = 0; u < kPF; ++u) {
       const long long cu = c + u;
@@ -425,7 +504,11 @@ __global__ __launch_bounds__(64 * kNP) void k3_coarse(SmoothArgs a, Plan3 p) {
 #pragma unroll
   for (int u = 0; u < kPM; ++u)
     if (c1 - 1 - u >= cl) load_map(c1 - 1 - u, Gr[u], gr[u]);
+#ifdef EKS_K3C_SKIP_E  // timing experiment only
+  for (long long cb0 = c1 - 1; cb0 >= c1; cb0 -= kPM) {
+#else
   for (long long cb0 = c1 - 1; cb0 >= cl; cb0 -= kPM) {
+#endif
 #pragma unroll
     for (int u = 0; u < kPM; ++u) {
       const long long cb = cb0 - u;
@@ -680,18 +763,29 @@ __global__ __launch_bounds__(kBlock) void k3_final(SmoothArgs a, Plan3 p) {
 // step (LDS for the early sub-chunks, registers for the last one) instead of
 // (y, ev), so the backward sweep computes the RTS gains without re-running
 // the filter (one filter pass per step instead of 1.5).
-template <int R, int N, int E, typename T, typename YT, bool AI, bool CI, int LS>
-__global__ __launch_bounds__(kBlock) void k3_final_s(SmoothArgs a, Plan3 p) {
+template <int R, int N, int E, typename T, typename YT, bool AI, bool CI, int LS, bool WALK>
+__global__ __launch_bounds__(kBlock) EKS_K3_WPE void k3_final_s(SmoothArgs a, Plan3 p) {
   constexpr int KS = R + Sym<R>::len;
   constexpr int D = EKS_K3_DF;
   constexpr int NST = (kNS - 1) * LS;  // steps kept in LDS
   __shared__ double fs[NST][KS][kBlock];
-  Lane<true> ln;
   const long long B = a.B, TT = a.T;
-  if (!ln.init(B, p.NCf)) return;
-  const long long c = ln.c;
-  const unsigned b = ln.b;
   const int tid = threadIdx.x;
+  long long c;
+  unsigned b;
+  if constexpr (WALK) {  // block = the kNF fine chunks of one coarse chunk x 64 trajectories
+    static_assert(64 * kNF == kBlock, "one wave per fine chunk of a coarse chunk");
+    const long long ng = (B + 63) / 64;
+    const long long cc = blockIdx.x / ng;
+    b = (unsigned)((blockIdx.x - cc * ng) * 64 + (tid & 63));
+    c = cc * kNF + (tid >> 6);
+    if ((long long)b >= B || c >= p.NCf) return;
+  } else {
+    Lane<true> ln;
+    if (!ln.init(B, p.NCf)) return;
+    c = ln.c;
+    b = ln.b;
+  }
   Model<R, N> md;
   md.load(a.params + (long long)b * ParamLayout<R, N>::len, c == 0);
   const long long s = c * p.L, e = min(TT, s + p.L);
@@ -699,25 +793,97 @@ __global__ __launch_bounds__(kBlock) void k3_final_s(SmoothArgs a, Plan3 p) {
   const int nsub = (int)((e - s + LS - 1) / LS);
   typename SrcOf<E, N, T, D>::type src;
   src.init(a, b);
+  constexpr int LF = kNS * LS;
+  const bool full = EKS_K3_FULLPATH && e - s == LF;  // all chunks but a trajectory's last: no runtime guards
+  if (full) {
 #pragma unroll
-  for (int q = 0; q < D; ++q)
-    if (s + q < e) src.fetch(q, s + q);
-  double m[R], P[R][R];
-  if (c == 0) {
+    for (int q = 0; q < D; ++q) src.fetch(q, s + q);
+  } else {
 #pragma unroll
-    for (int i = 0; i < R; ++i) {
-      m[i] = md.m0[i];
+    for (int q = 0; q < D; ++q)
+      if (s + q < e) src.fetch(q, s + q);
+  }
+  double m[R], P[R][R], msE[R];
+  bool ok = true;
+  if constexpr (WALK) {
+    // the fine walk of P3, redundantly per wave (the block's 4 waves read the
+    // same 4 elements: one HBM fetch, L1/L2 hits after): filtered state
+    // entering this fine chunk, and the smoothed mean at its last step = the
+    // later fine chunks' RTS maps applied to the coarse boundary mean
+    const long long cc = c / kNF, f0 = cc * kNF, f1 = min(p.NCf, f0 + kNF);
+    const int w = (int)(c - f0);
+    Elem<R> El[kNF];
 #pragma unroll
-      for (int j = 0; j < R; ++j) P[i][j] = md.S0[i][j];
+    for (int j = 0; j < kNF; ++j)
+      if (f0 + j < f1) load_elem_pl<R>((const double *)(a.ws + p.fel_off), f0 + j, B, b, El[j]);
+    double wm[R], wP[R][R], G[kNF][R][R], g[kNF][R];
+    if (cc > 0) load_state_pl<R>((const double *)(a.ws + p.ccs_off), cc * KS, B, b, wm, wP);
+#pragma unroll
+    for (int j = 0; j < kNF; ++j) {
+      const long long f = f0 + j;
+      if (f < f1) {
+        if (j == w) {
+#pragma unroll
+          for (int i = 0; i < R; ++i) {
+            m[i] = wm[i];
+#pragma unroll
+            for (int k = 0; k < R; ++k) P[i][k] = wP[i][k];
+          }
+        }
+        if (f == 0) {  // the first chunk's element is its end state
+#pragma unroll
+          for (int i = 0; i < R; ++i) {
+            wm[i] = El[j].bb[i];
+#pragma unroll
+            for (int k = 0; k < R; ++k) wP[i][k] = El[j].Cb[i][k];
+          }
+        } else {
+          bool okw = compose_state_rts<R>(wm, wP, El[j], G[j], g[j]);
+          if (j > w) ok = ok && okw;  // maps this chunk does not use are checked elsewhere
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+      msE[i] = last ? 0.0 : pl((const double *)(a.ws + p.cms_off), (cc + 1) * R + i, B, b);
+#pragma unroll
+    for (int j = kNF - 1; j >= 0; --j) {
+      if (j > w && f0 + j < f1) {
+        double nx[R];
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+          double sm = g[j][i];
+#pragma unroll
+          for (int k = 0; k < R; ++k) sm = fma(G[j][i][k], msE[k], sm);
+          nx[i] = sm;
+        }
+#pragma unroll
+        for (int i = 0; i < R; ++i) msE[i] = nx[i];
+      }
+    }
+    if (c == 0) {
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        m[i] = md.m0[i];
+#pragma unroll
+        for (int k = 0; k < R; ++k) P[i][k] = md.S0[i][k];
+      }
     }
   } else {
-    load_state_pl<R>((const double *)(a.ws + p.fcs_off), c * KS, B, b, m, P);
-  }
-  double msE[R];
+    if (c == 0) {
 #pragma unroll
-  for (int i = 0; i < R; ++i)
-    msE[i] = last ? 0.0 : pl((const double *)(a.ws + p.fms_off), c * R + i, B, b);
-  bool ok = true;
+      for (int i = 0; i < R; ++i) {
+        m[i] = md.m0[i];
+#pragma unroll
+        for (int j = 0; j < R; ++j) P[i][j] = md.S0[i][j];
+      }
+    } else {
+      load_state_pl<R>((const double *)(a.ws + p.fcs_off), c * KS, B, b, m, P);
+    }
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+      msE[i] = last ? 0.0 : pl((const double *)(a.ws + p.fms_off), c * R + i, B, b);
+  }
   NllAcc acc;
   double Mr[LS][KS];  // filtered states of the last sub-chunk
   auto pack = [&](double (&dst)[KS]) {
@@ -729,28 +895,40 @@ __global__ __launch_bounds__(kBlock) void k3_final_s(SmoothArgs a, Plan3 p) {
 #pragma unroll
       for (int j = i; j < R; ++j) dst[k++] = P[i][j];
   };
+  auto fwd = [&](auto fullc) {
+    constexpr bool FULL = decltype(fullc)::value;
 #pragma unroll
-  for (int i = 0; i < kNS * LS; ++i) {
-    const long long t = s + i;
-    const int k = i / LS, q = i % LS;
-    if (t < e) {
-      double avg[N], rv[N], y[N];
-      src.get(i % D, avg, rv);
-      if (t + D < e) src.fetch(i % D, t + D);
+    for (int i = 0; i < LF; ++i) {
+      const long long t = s + i;
+      const int k = i / LS, q = i % LS;
+      if (FULL || t < e) {
+        double avg[N], rv[N], y[N];
+        src.get(i % D, avg, rv);
+        if (FULL) {
+          if (i + D < LF) src.fetch(i % D, t + D);
+        } else if (t + D < e) {
+          src.fetch(i % D, t + D);
+        }
+        EKS_PIN_LOADS();
 #pragma unroll
-      for (int j = 0; j < N; ++j) y[j] = avg[j] - md.off[j];
-      if (t > 0) kf_predict<R, AI>(m, P, md.A, md.Q);
-      kf_update<R, N, CI>(m, P, md.C, y, rv, acc, ok);
-      if (k == nsub - 1) {
-        pack(Mr[q]);
-      } else if (k < kNS - 1) {
-        double st[KS];
-        pack(st);
+        for (int j = 0; j < N; ++j) y[j] = avg[j] - md.off[j];
+        if (t > 0) kf_predict<R, AI>(m, P, md.A, md.Q);
+        kf_update<R, N, CI>(m, P, md.C, y, rv, acc, ok);
+        if (FULL ? k == kNS - 1 : k == nsub - 1) {
+          pack(Mr[q]);
+        } else if (k < kNS - 1) {
+          double st[KS];
+          pack(st);
 #pragma unroll
-        for (int u = 0; u < KS; ++u) fs[i][u][tid] = st[u];
+          for (int u = 0; u < KS; ++u) fs[i][u][tid] = st[u];
+        }
       }
     }
-  }
+  };
+  if (full)
+    fwd(std::true_type{});
+  else
+    fwd(std::false_type{});
   if (a.nll) pl((double *)(a.ws + p.nllp_off), c, B, b) = acc.value((double)(e - s) * N);
   double *outb = a.out + (long long)b * a.ob;
   const bool vec2 = N == 2 && a.oj == 1 && ((a.ob | a.ot) & 1) == 0 &&
@@ -865,17 +1043,23 @@ int launch_algo3(const SmoothArgs &a) {
     int rc;
     prof_call_begin();
     prof_mark(a.stream, "k3_elem");
-    hipLaunchKernelGGL((k3_elem<R, N, EE, Tp, AI, CI>), dim3(g1), dim3(64 * kNF), 0, a.stream, a, p);
+    hipLaunchKernelGGL((k3_elem<R, N, EE, Tp, AI, CI>), dim3(g1), dim3(64 * kWV), 0, a.stream, a, p);
     if ((rc = check_launch("k3_elem"))) return rc;
     prof_mark(a.stream, "k3_coarse");
     hipLaunchKernelGGL((k3_coarse<R>), dim3(grid_for(a.B, 64)), dim3(64 * kNP), 0, a.stream, a, p);
     if ((rc = check_launch("k3_coarse"))) return rc;
+#if EKS_K3_MERGED
+    prof_mark(a.stream, "k3_final");
+    hipLaunchKernelGGL((k3_final_s<R, N, EE, Tp, YT, AI, CI, LS, true>), dim3(g1), dim3(kBlock), 0,
+                       a.stream, a, p);
+#else
     prof_mark(a.stream, "k3_fine");
     hipLaunchKernelGGL((k3_fine<R>), dim3(g3), dim3(kBlock), 0, a.stream, a, p);
     if ((rc = check_launch("k3_fine"))) return rc;
     prof_mark(a.stream, "k3_final");
-    hipLaunchKernelGGL((EKS_K3_FINAL<R, N, EE, Tp, YT, AI, CI, LS>), dim3(g4), dim3(kBlock), 0,
+    hipLaunchKernelGGL((k3_final_s<R, N, EE, Tp, YT, AI, CI, LS, false>), dim3(g4), dim3(kBlock), 0,
                        a.stream, a, p);
+#endif
     if ((rc = check_launch("k3_final"))) return rc;
     if (a.nll) {
       prof_mark(a.stream, "k3_nll");
