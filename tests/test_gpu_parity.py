@@ -697,3 +697,25 @@ def test_fit_yev_handoff_bit_exact(torch, kind, V, E, dtype, mode, algo):
     assert torch.equal(a, b)
     y32 = dtype == "f32" and mode == "median" and E in (3, 5)
     assert yev.code == (2 if y32 else 3)
+
+
+def test_algo3_batch_slices_bit_identical(torch):
+    """algo 3's chunking (16-frame fine chunks, 64-frame coarse chunks, 8
+    scan parts) depends on T only, never on the batch: smoothing a slice of
+    the trajectories gives bit-identical results to smoothing all of them
+    (what sharding the batch over GPUs relies on)."""
+    from eks_amd import _lib, batch, synthetic
+    rng = np.random.default_rng(21)
+    B, T, E = 1100, 600, 5
+    st = synthetic.singleview_obs(rng, E, T, K=B).transpose(2, 0, 1, 3).astype(np.float32)
+    d = batch.make_time_major(st, dtype=np.float32)               # (B, T, E, 2) view
+    params = batch.fit(d, kind="singleview", n=2, r=2, smooth_param=0.01, quantile_keep=25)[0]
+    flags = _lib.EKS_MODEL_A_IDENTITY | _lib.EKS_MODEL_C_IDENTITY
+    full = batch.smooth(d, params, n=2, r=2, algo=3, flags=flags, want_ms=True, want_nll=True)
+    assert (full["status"] == 0).all()
+    for lo, hi in ((0, 70), (600, 700), (1030, 1100)):           # first half, boundary, second half
+        part = batch.smooth(d[lo:hi], params[lo:hi].contiguous(), n=2, r=2, algo=3, flags=flags,
+                            want_ms=True, want_nll=True)
+        assert torch.equal(part["out"], full["out"][lo:hi]), (lo, hi)
+        assert torch.equal(part["ms"], full["ms"][lo:hi]), (lo, hi)
+        assert torch.equal(part["nll"], full["nll"][lo:hi]), (lo, hi)
