@@ -13,19 +13,19 @@
 //                filtering element (planes); the 4 waves of a block are 4
 //                consecutive fine chunks of 64 trajectories, composed (LDS
 //                tree) into one coarse (64-step) element
-//  P2 k3_coarse  8 waves per 64 trajectories over the coarse elements
-//                (parallel scan through LDS): filtered state entering each
-//                coarse chunk, coarse RTS maps, then the smoothed mean at
-//                every coarse boundary
+//  P2 k3_coarse  8 waves (x S sub-parts) per 64 (/ S) trajectories over the
+//                coarse elements (parallel scan, shuffles + LDS): filtered
+//                state entering each coarse chunk, coarse RTS maps, then the
+//                smoothed mean at every coarse boundary
 //  P3 k3_fine    one lane per (coarse chunk, trajectory): the same over its 4
 //                fine elements -> filtered state entering / smoothed mean at
 //                the last step of every fine chunk
-//  P4 k3_final   fine chunk per lane: members again -> ensemble -> filter from
-//                the exact start state; the first 8-step sub-chunk's (y, ev)
-//                are kept in LDS, the second's RTS gains (J_t, d_t) in
-//                registers; RTS backwards from the chunk's known last-step
-//                mean, then the first sub-chunk is re-run from LDS; writes
-//                C ms + offset (and ms / the chunk's NLL share)
+//  P4 k3_final_s fine chunk per lane: members again -> ensemble -> filter
+//                from the exact start state; the filtered states of the first
+//                8-step sub-chunk are kept in LDS, the second's in registers;
+//                RTS backwards from the chunk's known last-step mean (no
+//                filter re-run); writes C ms + offset (and ms / the chunk's
+//                NLL share).  k3_final is the earlier (y, ev)-stash variant.
 //
 // HBM bytes per keypoint-timestep (single view, E = 5): P1 40 + 7 (fine
 // elements) + 1.75 (coarse), P2 ~2, P3 7 + 3.5, P4 40 + 3.5 + 16 ~= 121,
@@ -348,20 +348,53 @@ __global__ __launch_bounds__(64 * kWV) EKS_K3E_WPE void k3_elem(SmoothArgs a, Pl
 #endif
 constexpr int kNP = EKS_K3_NP;
 
+// Small batches (an 8-GPU shard) leave most CUs idle with one trajectory per
+// lane, and the chains are latency bound: S > 1 splits every wave into S
+// sub-parts of TW = 64 / S trajectories (TW * 8-byte row segments), i.e.
+// kNP * S parts per trajectory, each S times shorter.  Inside a wave the
+// part aggregates are scanned with shuffles; across waves through LDS as
+// above.  The partition depends on S, so results for different S agree to
+// rounding, not bit for bit.
 template <int R>
+EKS_DEV Elem<R> shfl_up_elem(const Elem<R> &e, int d) {
+  double v[Elem<R>::len];
+  e.store(v, 1);
+#pragma unroll
+  for (int k = 0; k < Elem<R>::len; ++k) v[k] = __shfl_up(v[k], d, 64);
+  Elem<R> o;
+  o.load(v, 1);
+  return o;
+}
+
+// S from a sweep at T = 10 000 (tools/gpu_ssweep.sh): k3_coarse at
+// B = 2 176 (one 8-GPU shard of config 4) S = 1/2/4/8: 0.083 / 0.053 / 0.040 /
+// 0.066 ms; at B = 8 704: 0.106 / 0.125 / 0.119 / 0.180 ms.  EKS_K3_S
+// overrides.
+inline int coarse_subparts(long long B) {
+  if (const char *s = getenv("EKS_K3_S")) {
+    const int v = atoi(s);
+    if (v == 1 || v == 2 || v == 4 || v == 8) return v;
+  }
+  return B <= 4608 ? 4 : 1;
+}
+
+template <int R, int S>
 __global__ __launch_bounds__(64 * kNP) void k3_coarse(SmoothArgs a, Plan3 p) {
   constexpr int KS = R + Sym<R>::len, MP = R * R + R, EL = Elem<R>::len;
-  __shared__ double shE[kNP][EL][64];
-  __shared__ double shF[kNP][MP][64];
-  __shared__ double shM[R][64];
+  constexpr int TW = 64 / S, NPT = kNP * S;
+  __shared__ double shE[kNP][EL][TW];
+  __shared__ double shF[NPT][MP][TW];
+  __shared__ double shM[R][TW];
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int sub = l / TW, tl = l % TW;
+  const int gp = w * S + sub;  // part index
   const long long B = a.B;
-  const long long bl = blockIdx.x * 64LL + l;
+  const long long bl = blockIdx.x * (long long)TW + tl;
   const bool live = bl < B;
   const unsigned b = live ? (unsigned)bl : 0u;  // dead lanes shadow trajectory 0, store nothing
   const long long NC = p.NCc;
-  const long long q = (NC + kNP - 1) / kNP;
-  const long long c0 = min(NC, (long long)w * q), c1 = min(NC, c0 + q);
+  const long long q = (NC + NPT - 1) / NPT;
+  const long long c0 = min(NC, (long long)gp * q), c1 = min(NC, c0 + q);
   const double *cel = (const double *)(a.ws + p.cel_off);
   double *ccs = (double *)(a.ws + p.ccs_off);
   double *cmap = (double *)(a.ws + p.cmap_off);
@@ -390,27 +423,47 @@ __global__ __launch_bounds__(64 * kNP) void k3_coarse(SmoothArgs a, Plan3 p) {
       }
     }
   }
-  agg.store(&shE[w][0][l], 64);
+  // (b) filtered state entering c0.  Inside the wave: inclusive scan of the S
+  // part aggregates, excl = the wave's parts before this one composed.
+  Elem<R> excl;
+  if constexpr (S > 1) {
+#pragma unroll
+    for (int k = 1; k < S; k <<= 1) {
+      const Elem<R> o = shfl_up_elem<R>(agg, TW * k);
+      if (sub >= k) {
+        Elem<R> t;
+        ok = compose_elem<R>(o, agg, t) && ok;
+        agg = t;
+      }
+    }
+    excl = shfl_up_elem<R>(agg, TW);
+  }
+  if (sub == S - 1) agg.store(&shE[w][0][tl], TW);  // the wave's aggregate
   __syncthreads();
-  // (b) filtered state entering c0
   double m[R], P[R][R];
-  {
-    Elem<R> e0;
-    e0.load(&shE[0][0][l], 64);
+  auto set_state = [&](const Elem<R> &e) {  // an element starting at the prior is a state
 #pragma unroll
     for (int i = 0; i < R; ++i) {
-      m[i] = e0.bb[i];
+      m[i] = e.bb[i];
 #pragma unroll
-      for (int j = 0; j < R; ++j) P[i][j] = e0.Cb[i][j];
+      for (int j = 0; j < R; ++j) P[i][j] = e.Cb[i][j];
     }
-  }
-  for (int v = 1; v < w; ++v) {
-    Elem<R> ev;
-    ev.load(&shE[v][0][l], 64);
-    ok = compose_state<R>(m, P, ev) && ok;
+  };
+  if (w > 0) {
+    Elem<R> e0;
+    e0.load(&shE[0][0][tl], TW);
+    set_state(e0);
+    for (int v = 1; v < w; ++v) {
+      Elem<R> ev;
+      ev.load(&shE[v][0][tl], TW);
+      ok = compose_state<R>(m, P, ev) && ok;
+    }
+    if (sub > 0) ok = compose_state<R>(m, P, excl) && ok;
+  } else if (sub > 0) {
+    set_state(excl);
   }
   long long c = c0;
-  if (w == 0) {  // coarse chunk 0 is a state: its end state is the walk's start
+  if (gp == 0) {  // coarse chunk 0 is a state: its end state is the walk's start
     Elem<R> e0;
     load_elem_pl<R>(cel, 0, B, b, e0);
 #pragma unroll
@@ -462,27 +515,27 @@ __global__ __launch_bounds__(64 * kNP) void k3_coarse(SmoothArgs a, Plan3 p) {
 #pragma unroll
     for (int i = 0; i < R; ++i)
 #pragma unroll
-      for (int j = 0; j < R; ++j) shF[w][k++][l] = F.G[i][j];
+      for (int j = 0; j < R; ++j) shF[gp][k++][tl] = F.G[i][j];
 #pragma unroll
-    for (int i = 0; i < R; ++i) shF[w][k++][l] = F.g[i];
+    for (int i = 0; i < R; ++i) shF[gp][k++][tl] = F.g[i];
   }
-  if (w == plast)
+  if (gp == plast)
 #pragma unroll
     for (int i = 0; i < R; ++i) {
-      shM[i][l] = m[i];
+      shM[i][tl] = m[i];
       if (live) pl(cms, NC * R + i, B, b) = m[i];
     }
   __syncthreads();
   double ms[R];
 #pragma unroll
-  for (int i = 0; i < R; ++i) ms[i] = shM[i][l];
-  for (int v = kNP - 1; v > w; --v) {
+  for (int i = 0; i < R; ++i) ms[i] = shM[i][tl];
+  for (int v = plast; v > gp; --v) {  // parts after plast are empty (identity maps)
     double nx[R];
 #pragma unroll
     for (int i = 0; i < R; ++i) {
-      double sm = shF[v][R * R + i][l];
+      double sm = shF[v][R * R + i][tl];
 #pragma unroll
-      for (int k = 0; k < R; ++k) sm = fma(shF[v][i * R + k][l], ms[k], sm);
+      for (int k = 0; k < R; ++k) sm = fma(shF[v][i * R + k][tl], ms[k], sm);
       nx[i] = sm;
     }
 #pragma unroll
@@ -1046,7 +1099,12 @@ int launch_algo3(const SmoothArgs &a) {
     hipLaunchKernelGGL((k3_elem<R, N, EE, Tp, AI, CI>), dim3(g1), dim3(64 * kWV), 0, a.stream, a, p);
     if ((rc = check_launch("k3_elem"))) return rc;
     prof_mark(a.stream, "k3_coarse");
-    hipLaunchKernelGGL((k3_coarse<R>), dim3(grid_for(a.B, 64)), dim3(64 * kNP), 0, a.stream, a, p);
+    switch (coarse_subparts(a.B)) {
+      case 8: hipLaunchKernelGGL((k3_coarse<R, 8>), dim3(grid_for(a.B, 8)), dim3(64 * kNP), 0, a.stream, a, p); break;
+      case 4: hipLaunchKernelGGL((k3_coarse<R, 4>), dim3(grid_for(a.B, 16)), dim3(64 * kNP), 0, a.stream, a, p); break;
+      case 2: hipLaunchKernelGGL((k3_coarse<R, 2>), dim3(grid_for(a.B, 32)), dim3(64 * kNP), 0, a.stream, a, p); break;
+      default: hipLaunchKernelGGL((k3_coarse<R, 1>), dim3(grid_for(a.B, 64)), dim3(64 * kNP), 0, a.stream, a, p);
+    }
     if ((rc = check_launch("k3_coarse"))) return rc;
 #if EKS_K3_MERGED
     prof_mark(a.stream, "k3_final");

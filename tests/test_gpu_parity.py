@@ -700,10 +700,10 @@ def test_fit_yev_handoff_bit_exact(torch, kind, V, E, dtype, mode, algo):
 
 
 def test_algo3_batch_slices_bit_identical(torch):
-    """algo 3's chunking (16-frame fine chunks, 64-frame coarse chunks, 8
-    scan parts) depends on T only, never on the batch: smoothing a slice of
-    the trajectories gives bit-identical results to smoothing all of them
-    (what sharding the batch over GPUs relies on)."""
+    """algo 3's chunking (16-frame fine chunks, 64-frame coarse chunks, 8 * S
+    scan parts) depends on T and the coarse scan's sub-part count S only:
+    smoothing a slice of the trajectories with the same S (here 4 for every
+    B <= 4608) gives bit-identical results to smoothing all of them."""
     from eks_amd import _lib, batch, synthetic
     rng = np.random.default_rng(21)
     B, T, E = 1100, 600, 5
@@ -719,3 +719,27 @@ def test_algo3_batch_slices_bit_identical(torch):
         assert torch.equal(part["out"], full["out"][lo:hi]), (lo, hi)
         assert torch.equal(part["ms"], full["ms"][lo:hi]), (lo, hi)
         assert torch.equal(part["nll"], full["nll"][lo:hi]), (lo, hi)
+
+
+@pytest.mark.parametrize("S", [1, 2, 4, 8])
+def test_algo3_coarse_subparts(torch, S, monkeypatch):
+    """The coarse scan's sub-part count S (picked from B; EKS_K3_S pins it)
+    changes the partition of the coarse chunks into scan parts: every S must
+    reproduce the sequential recursion, including parts that are empty
+    (T short enough that some of the 8 * S parts hold no coarse chunk)."""
+    from eks_amd import _lib, batch, synthetic
+    rng = np.random.default_rng(40 + S)
+    B, E = 300, 5
+    flags = _lib.EKS_MODEL_A_IDENTITY | _lib.EKS_MODEL_C_IDENTITY
+    for T in (2000, 700, 64, 17):       # 32, 11, 1 and 1 coarse chunks
+        st = synthetic.singleview_obs(rng, E, T, K=B).transpose(2, 0, 1, 3).astype(np.float32)
+        d = batch.make_time_major(st, dtype=np.float32)
+        params = batch.fit(d, kind="singleview", n=2, r=2, smooth_param=0.01, quantile_keep=25)[0]
+        ref = batch.smooth(d, params, n=2, r=2, algo=1, flags=flags, want_ms=True, want_nll=True)
+        monkeypatch.setenv("EKS_K3_S", str(S))
+        got = batch.smooth(d, params, n=2, r=2, algo=3, flags=flags, want_ms=True, want_nll=True)
+        monkeypatch.delenv("EKS_K3_S")
+        assert (got["status"] == 0).all(), T
+        assert float((got["out"] - ref["out"]).abs().max()) < 1e-8, T
+        assert float((got["ms"] - ref["ms"]).abs().max()) < 1e-8, T
+        torch.testing.assert_close(got["nll"], ref["nll"], rtol=1e-10, atol=0)
