@@ -407,11 +407,7 @@ __global__ __launch_bounds__(64 * kNP) void k3_coarse(SmoothArgs a, Plan3 p) {
 #pragma unroll
   for (int u = 0; u < kPF; ++u)
     if (c0 + u < c1) load_elem_pl<R>(cel, c0 + u, B, b, ring[u]);
-#ifdef EKS_K3C_SKIP_A  // timing experiment only
-  for (long long c = c0; c < c0; c += kPF) {
-#else
   for (long long c = c0; c < c1; c += kPF) {
-#endif
 #pragma unroll
     for (int u = 0; u < kPF; ++u) {
       if (c + u < c1) {
@@ -480,11 +476,7 @@ __global__ __launch_bounds__(64 * kNP) void k3_coarse(SmoothArgs a, Plan3 p) {
 #pragma unroll
   for (int u = 0; u < kPF; ++u)
     if (c + u < c1) load_elem_pl<R>(cel, c + u, B, b, ring[u]);
-#ifdef EKS_K3C_SKIP_C  // timing experiment only
-  for (; c < c0; c += kPF) {
-#else
   for (; c < c1; c += kPF) {
-#endif
 #pragma unroll
     for (int u = 0; u < kPF; ++u) {
       const long long cu = c + u;
@@ -557,11 +549,7 @@ __global__ __launch_bounds__(64 * kNP) void k3_coarse(SmoothArgs a, Plan3 p) {
 #pragma unroll
   for (int u = 0; u < kPM; ++u)
     if (c1 - 1 - u >= cl) load_map(c1 - 1 - u, Gr[u], gr[u]);
-#ifdef EKS_K3C_SKIP_E  // timing experiment only
-  for (long long cb0 = c1 - 1; cb0 >= c1; cb0 -= kPM) {
-#else
   for (long long cb0 = c1 - 1; cb0 >= cl; cb0 -= kPM) {
-#endif
 #pragma unroll
     for (int u = 0; u < kPM; ++u) {
       const long long cb = cb0 - u;
