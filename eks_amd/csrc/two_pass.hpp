@@ -366,16 +366,17 @@ EKS_DEV Elem<R> shfl_up_elem(const Elem<R> &e, int d) {
   return o;
 }
 
-// S from a sweep at T = 10 000 (tools/gpu_ssweep.sh): k3_coarse at
-// B = 2 176 (one 8-GPU shard of config 4) S = 1/2/4/8: 0.083 / 0.053 / 0.040 /
-// 0.066 ms; at B = 8 704: 0.106 / 0.125 / 0.119 / 0.180 ms.  EKS_K3_S
-// overrides.
+// S from a sweep at T = 10 000 (tools/gpu_ssweep.sh), k3_coarse ms for
+// S = 1 / 2 / 4 (/ 8):  B = 2 176 (one 8-GPU shard of config 4): 0.083 /
+// 0.053 / 0.040 / 0.066;  B = 4 352: 0.086 / 0.059 / 0.076;  B = 6 528:
+// 0.090 / 0.071 / 0.082;  B = 8 704: 0.106 / 0.125 / 0.119 / 0.180.
+// EKS_K3_S overrides.
 inline int coarse_subparts(long long B) {
   if (const char *s = getenv("EKS_K3_S")) {
     const int v = atoi(s);
     if (v == 1 || v == 2 || v == 4 || v == 8) return v;
   }
-  return B <= 4608 ? 4 : 1;
+  return B <= 3072 ? 4 : B <= 7680 ? 2 : 1;
 }
 
 template <int R, int S>

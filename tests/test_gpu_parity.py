@@ -703,7 +703,7 @@ def test_algo3_batch_slices_bit_identical(torch):
     """algo 3's chunking (16-frame fine chunks, 64-frame coarse chunks, 8 * S
     scan parts) depends on T and the coarse scan's sub-part count S only:
     smoothing a slice of the trajectories with the same S (here 4 for every
-    B <= 4608) gives bit-identical results to smoothing all of them."""
+    B <= 3072) gives bit-identical results to smoothing all of them."""
     from eks_amd import _lib, batch, synthetic
     rng = np.random.default_rng(21)
     B, T, E = 1100, 600, 5

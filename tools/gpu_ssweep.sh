@@ -3,8 +3,8 @@
 set -o pipefail
 mkdir -p gpurun_out
 export PYTHONDONTWRITEBYTECODE=1
-for nv in 128 512; do
-  for s in 1 2 4 8; do
+for nv in ${SS_VIDEOS:-128 512}; do
+  for s in ${SS_S:-1 2 4 8}; do
     EKS_K3_S=$s timeout -k 10 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --videos $nv > gpurun_out/s_${nv}_$s.log 2>&1 || exit $?
     python - gpurun_out/s_${nv}_$s.log "v=$nv S=$s" <<'PY'
 import json, sys
