@@ -63,11 +63,13 @@ def parse():
     ap.add_argument("--quantile-keep", type=float, default=25.0)
     ap.add_argument("--seed", type=int, default=None)
     ap.add_argument("--algo", type=int, default=0, help="eks_smooth algo (0 auto)")
-    ap.add_argument("--cpu-sample", type=int, default=None,
-                    help="trajectories timed on the CPU oracle (rank 0, N=1)")
+    ap.add_argument("--cpu-cores", type=int, default=None,
+                    help="processes of the all-core CPU baseline (default: the affinity mask, "
+                         "capped by OMP_NUM_THREADS)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--gather", action="store_true",
-                    help="config 4: after timing, gather all outputs to rank 0 (RCCL) once")
+    ap.add_argument("--no-gather", action="store_true",
+                    help="config 4, N > 1: skip the final gather of all outputs to rank 0 "
+                         "(RCCL), timed once after the throughput loop")
     ap.add_argument("--timeshard", action="store_true",
                     help="config 5: split the frames over the ranks (eks_amd.timeshard: two "
                          "all_gathers of per-segment aggregates) instead of replicas")
@@ -123,34 +125,115 @@ def ensemble_dev(torch, obs_view, mode="median"):
     return preds, var
 
 
-def cpu_pipeline(stack, fit_fn, mode="median"):
-    """One trajectory through the CPU oracle, phases timed separately:
-    ensemble, model fit, forward + backward + projection.  Returns
-    (out, t_ensemble, t_fit, t_smooth)."""
+# ---------------------------------------------------------------------------
+# CPU baseline: the numpy oracle (oracle/eks_oracle.py) on the host cores,
+# 1 core and one process per core, BLAS single-threaded in every process
+# ---------------------------------------------------------------------------
+def cpu_cores() -> int:
+    """Cores the all-core baseline uses: the affinity mask, capped by the
+    box's CPU share (OMP_NUM_THREADS / EKS_CPU_CORES, read before this
+    process pins its own BLAS to one thread)."""
+    n = len(os.sched_getaffinity(0))
+    cap = os.environ.get("EKS_CPU_CORES") or os.environ.get("OMP_NUM_THREADS")
+    if cap and cap.isdigit() and int(cap) > 0:
+        n = min(n, int(cap))
+    return max(1, n)
+
+
+def _cpu_model(O, task):
+    """Untimed model fit of one task, from its own ensemble."""
+    kind, stack, args = task
+    if kind == "nll":           # the model is given (a sweep candidate)
+        return args
+    preds, ev = O.ensemble_array(stack)
+    fit = {"singleview": O.singleview_params, "multicam": O.multicam_params,
+           "pupil": O.pupil_params}[kind]
+    return fit(preds, ev, *args)
+
+
+def _cpu_hot(O, task, p):
+    """The GPU step's scope for one task on the CPU: ensemble ->
+    filtering_pass -> smooth_backward -> projection (eks/ensemble_kalman.py:
+    4-164), or ensemble -> innovation NLL for a sweep candidate."""
     import numpy as np
-    from oracle import eks_oracle as O
-    t0 = time.perf_counter()
-    preds, ev = O.ensemble_array(stack, mode)
-    t1 = time.perf_counter()
-    p = fit_fn(preds, ev)
-    t2 = time.perf_counter()
-    y = p["y"]
-    R = np.eye(y.shape[1])
-    mf, Vf, S = O.filtering_pass(y, p["m0"], p["S0"], p["C"], R, p["A"], p["Q"], ev)
+    kind, stack, _ = task
+    preds, ev = O.ensemble_array(stack)
+    y = preds - p["means"]
+    if kind == "nll":
+        return O.compute_nll(y, p["m0"], p["S0"], p["C"], p["A"], p["Q"], ev)
+    mf, Vf, S = O.filtering_pass(y, p["m0"], p["S0"], p["C"], np.eye(y.shape[1]), p["A"],
+                                 p["Q"], ev)
     ms, _, _ = O.smooth_backward(y, mf, Vf, S, p["A"])
-    out = ms @ p["C"].T + p["means"]
-    t3 = time.perf_counter()
-    return out, t1 - t0, t2 - t1, t3 - t2
+    return ms @ p["C"].T + p["means"]
 
 
-def cpu_result(units, outs_times, gpu_outs, sample):
-    """Hot-path rate (ensemble + filter + smoother + projection, the scope of
-    the GPU step) and end-to-end rate (plus the model fit) of the CPU runs."""
-    t_hot = sum(te + ts for _, te, _, ts in outs_times)
-    t_all = sum(te + tf + ts for _, te, tf, ts in outs_times)
-    diff = max(float(abs(o - g).max()) for (o, _, _, _), g in zip(outs_times, gpu_outs))
-    return dict(value=units / t_hot, e2e_value=units / t_all, dt=t_all, diff=diff,
-                sample=sample)
+def _cpu_worker(conn, barrier):
+    """One process of the all-core baseline: fit its tasks (untimed), wait
+    for every process, then time the hot path over its tasks."""
+    from oracle import eks_oracle as O
+    tasks = conn.recv()
+    models = [_cpu_model(O, t) for t in tasks]
+    barrier.wait()
+    t0 = time.perf_counter()
+    outs = [_cpu_hot(O, t, p) for t, p in zip(tasks, models)]
+    t1 = time.perf_counter()
+    conn.send((t0, t1, outs))
+    conn.close()
+
+
+def cpu_all_cores(tasks, cores):
+    """Tasks round-robin over ``cores`` spawned processes (one BLAS thread
+    each).  Returns (wall seconds of the timed hot phase: first start to last
+    end, outputs in task order)."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    cores = max(1, min(cores, len(tasks)))
+    saved = {k: os.environ.get(k) for k in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS",
+                                            "MKL_NUM_THREADS")}
+    for k in saved:
+        os.environ[k] = "1"
+    barrier = ctx.Barrier(cores)
+    procs, conns = [], []
+    try:
+        for i in range(cores):
+            parent, child = ctx.Pipe()
+            p = ctx.Process(target=_cpu_worker, args=(child, barrier), daemon=True)
+            p.start()
+            parent.send(tasks[i::cores])
+            procs.append(p)
+            conns.append(parent)
+        res = [c.recv() for c in conns]
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+        for p in procs:
+            p.join(timeout=60)
+    wall = max(r[1] for r in res) - min(r[0] for r in res)
+    outs = [None] * len(tasks)
+    for i, r in enumerate(res):
+        outs[i::cores] = r[2]
+    return wall, outs
+
+
+def cpu_one_core(tasks):
+    """Tasks in this process with one BLAS thread: (fit seconds, hot seconds
+    per task, outputs)."""
+    from threadpoolctl import threadpool_limits
+    from oracle import eks_oracle as O
+    t_fit = 0.0
+    t_hot, outs = [], []
+    with threadpool_limits(1):
+        for t in tasks:
+            f0 = time.perf_counter()
+            p = _cpu_model(O, t)
+            f1 = time.perf_counter()
+            outs.append(_cpu_hot(O, t, p))
+            t_fit += f1 - f0
+            t_hot.append(time.perf_counter() - f1)
+    return t_fit, t_hot, outs
 
 
 # ---------------------------------------------------------------------------
@@ -192,24 +275,23 @@ def workload_singleview(torch, a, dev, rank, world, config):
     def e2e_smooth():
         batch.smooth(yev["y"], params, n=2, r=2, out=out, status=status, algo=a.algo, flags=flags)
 
-    def cpu(n_traj):
+    def cpu_plan(cores):
         import numpy as np
-        from oracle import eks_oracle as O
-        host = obs_tm[:, :, :, :n_traj].cpu().numpy().astype(np.float64)  # (T, E, 2, b)
-        gpu = out[:n_traj].cpu().numpy()
-        fit_fn = lambda p, v: O.singleview_params(p, v, a.smooth_param, a.quantile_keep)  # noqa
-        runs = [cpu_pipeline(np.ascontiguousarray(np.transpose(host[..., b], (1, 0, 2))), fit_fn)
-                for b in range(n_traj)]
-        return cpu_result(n_traj * T, runs, gpu,
-                          f"{n_traj} trajectories x {T} frames of this workload (oracle "
-                          f"ensemble + filtering_pass + smooth_backward + projection, numpy, "
-                          f"1 thread; the single-view fit timed separately for end_to_end)")
+        n_all = min(B, max(2, cores * (8 if config == 4 else 1)))
+        host = obs_tm[:, :, :, :n_all].cpu().numpy().astype(np.float64)  # (T, E, 2, b)
+        gpu = out[:n_all].cpu().numpy()
+        tasks = [("singleview", np.ascontiguousarray(np.transpose(host[..., b], (1, 0, 2))),
+                  (a.smooth_param, a.quantile_keep)) for b in range(n_all)]
+        n_one = min(n_all, 32 if config == 4 else 2)
+        return dict(tasks=tasks, gpu={b: gpu[b] for b in range(n_all)},
+                    units_all=n_all * T, one=list(range(n_one)), units_one=n_one * T,
+                    what=f"{{n}} trajectories x {T} frames of this workload")
 
     desc = (f"config {config}: " + (f"batch of {a.videos} videos x " if config == 4 else "1 video x ")
             + f"{K} keypoints x {E} members x {T} frames, single-view EKS (ensemble median/var "
             f"-> forward KF -> RTS -> projection), float32 members, float64 recursions/outputs")
     return dict(step=step, fit_step=fit_step, e2e_smooth=e2e_smooth, status=status, units=B * T,
-                bytes_per_unit=E * 2 * 4 + 2 * 8, cpu=cpu, cpu_default=64 if config == 4 else 4, desc=desc,
+                bytes_per_unit=E * 2 * 4 + 2 * 8, cpu_plan=cpu_plan, desc=desc,
                 cfg=dict(videos=a.videos if config == 4 else 1, keypoints=K, members=E, frames=T,
                          trajectories_per_rank=B, smooth_param=a.smooth_param,
                          quantile_keep=a.quantile_keep),
@@ -249,20 +331,19 @@ def workload_multiview(torch, a, dev, rank, world):
     def e2e_smooth():
         batch.smooth(yev["y"], params, n=n, r=3, out=out, status=status, algo=a.algo, flags=flags)
 
-    def cpu(n_traj):
-        from oracle import eks_oracle as O
-        gpu = out[:n_traj].cpu().numpy()
-        fit_fn = lambda p, v: O.multicam_params(p, v, a.smooth_param, a.quantile_keep)  # noqa
-        runs = [cpu_pipeline(st[:, :, k, :].astype(np.float64), fit_fn) for k in range(n_traj)]
-        return cpu_result(n_traj * T, runs, gpu,
-                          f"{n_traj} keypoints x {T} frames x {V} cameras of this workload "
-                          f"(oracle ensemble + filtering_pass + smooth_backward + projection, "
-                          f"numpy, 1 thread; the PCA fit timed separately for end_to_end)")
+    def cpu_plan(cores):
+        n_all = min(K, max(2, cores))
+        gpu = out[:n_all].cpu().numpy()
+        tasks = [("multicam", st[:, :, k, :].astype(np.float64), (a.smooth_param, a.quantile_keep))
+                 for k in range(n_all)]
+        return dict(tasks=tasks, gpu={k: gpu[k] for k in range(n_all)},
+                    units_all=n_all * T, one=[0, 1], units_one=2 * T,
+                    what=f"{{n}} keypoints x {T} frames x {V} cameras of this workload")
 
     desc = (f"config 3: multiview PCA smoother, {V} cameras x {K} keypoints x {E} members x "
             f"{T} frames (r=3 latent, n=8), float32 members, float64 recursions/outputs")
     return dict(step=step, fit_step=fit_step, e2e_smooth=e2e_smooth, status=status,
-                units=K * T, bytes_per_unit=E * n * 4 + n * 8, cpu=cpu, cpu_default=5, desc=desc,
+                units=K * T, bytes_per_unit=E * n * 4 + n * 8, cpu_plan=cpu_plan, desc=desc,
                 cfg=dict(cameras=V, keypoints=K, members=E, frames=T,
                          smooth_param=a.smooth_param, quantile_keep=a.quantile_keep),
                 shape=(K, T, n, 3, E), key=f"config3-multiview-k{K}-e{E}-t{T}-n{world}")
@@ -319,21 +400,26 @@ def workload_pupil(torch, a, dev, rank, world):
                          algo=a.algo)
         state["best"], state["scores"], state["ms"] = best, scores, r["ms"]
 
-    def cpu(_n):
+    def cpu_plan(cores):
+        # the step's scope on a bounded prefix of Tc frames: every candidate's
+        # NLL (eks_amd batch.nll <-> oracle compute_nll) + smoothing the chosen one
         from oracle import eks_oracle as O
-        Tc = min(T, 200000)  # bounded sample: the first Tc frames, chosen model
+        Tc = min(T, 5000)
+        pre = np.ascontiguousarray(st[:, :Tc].astype(np.float64))
         b = int(state["best"].item())
-        Ab = cands[b]["A"]
-        run = cpu_pipeline(st[:, :Tc].astype(np.float64), lambda p, v: O.pupil_params(p, Ab))
+        tasks = [("nll", pre, dict(c, means=c["offset"])) for c in cands]
+        tasks.append(("pupil", pre, (cands[b]["A"],)))
         # the GPU output for the same prefix and model
-        pre = fit.pupil_model(O.ensemble_array(st[:, :Tc].astype(np.float64))[0], Ab)
-        pb = batch.pack_params(pre["m0"], pre["S0"], pre["A"], pre["Q"], pre["C"], pre["offset"],
+        pm = fit.pupil_model(O.ensemble_array(pre)[0], cands[b]["A"])
+        pb = batch.pack_params(pm["m0"], pm["S0"], pm["A"], pm["Q"], pm["C"], pm["offset"],
                                device=dev)
         g = batch.smooth(obs[:, :Tc], pb, n=8, r=3)["out"][0].cpu().numpy()
-        return cpu_result(4 * Tc, [run], [g],
-                          f"first {Tc} frames x 4 keypoints, best model (oracle ensemble + "
-                          f"filtering_pass + smooth_backward + projection, numpy, 1 thread); "
-                          f"the GPU step also scores {len(cands)} candidate models")
+        half = len(cands) // 2
+        return dict(tasks=tasks, gpu={len(cands): g}, units_all=4 * Tc, units_one=4 * Tc,
+                    one=[0, 1, len(cands)], weights=[half, half, 1],
+                    what=f"first {Tc} frames x 4 keypoints: NLL of all {len(cands)} candidate "
+                         f"models + smoothing the chosen one (1-core figure: 2 candidates "
+                         f"timed, x{half} each)")
 
     desc = (f"config 5: IBL-pupil smoother, {T} frames x 4 keypoints x {E} members (r=3 latent, "
             f"n=8): NLL sweep over {len(cands)} (diameter_s, com_s) models (filter-only, "
@@ -341,7 +427,7 @@ def workload_pupil(torch, a, dev, rank, world):
     if a.timeshard:
         desc += f"; frames split over {world} rank(s) (time-sharded scan)"
     return dict(step=step_timeshard if a.timeshard else step, status=status, units=4 * Tk,
-                bytes_per_unit=(32 * E + 88) / 4, cpu=cpu, cpu_default=1, desc=desc,
+                bytes_per_unit=(32 * E + 88) / 4, cpu_plan=cpu_plan, desc=desc,
                 timeshard=a.timeshard,
                 cfg=dict(frames=T, keypoints=4, members=E, candidates=len(cands)),
                 shape=(1, T, 8, 3, E),
@@ -352,7 +438,8 @@ def workload_pupil(torch, a, dev, rank, world):
 
 
 def load_pmc(workload_key):
-    path = os.path.join(HERE, "profiles", "pmc_latest.json")
+    # PMC summary of the same workload (tools/gpu_profile.sh -> tools/prof_summary.py)
+    path = os.path.join(HERE, "bench_pmc.json")
     if not os.path.exists(path):
         return None
     try:
@@ -362,8 +449,26 @@ def load_pmc(workload_key):
     return d if d.get("workload_key") == workload_key else None
 
 
+def launch_ranks(a) -> int:
+    """``--gpus N`` without a launcher: run N ranks of this script under
+    torch.distributed.run as a child process (started before this process
+    touches the GPU) and return its exit code."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={a.gpus}", "--master-addr", "127.0.0.1",
+           "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(a))
     import torch
     from eks_amd import _lib, dist
     from threadpoolctl import threadpool_limits
@@ -461,29 +566,54 @@ def main():
                    scope="eks_fit (ensemble, good-frame percentile, model fit; writes the "
                          "ensemble planes) + eks_smooth from those planes (members read once)")
 
+    # the one data-path collective of the batch job: every
+    # rank's smoothed (videos, T, K, 2) float64 block gathered to rank 0 over
+    # RCCL, timed once after the throughput loop, never inside ``value``
     gather_ms = None
-    if a.gather and world > 1 and a.config == 4:
-        torch.cuda.synchronize()
-        dist.barrier()
-        g0 = time.perf_counter()
+    gather_bytes = None
+    if not a.no_gather and world > 1 and a.config == 4:
         T, K = a.frames, a.keypoints
         nv = len(w["videos"])
         loc = w["out"].permute(1, 0, 2).reshape(T, nv, K, 2).permute(1, 0, 2, 3).contiguous()
-        full = dist.gather_to_rank0(loc, a.videos)
+        total_videos = nv * world if a.scaling == "weak" else a.videos
         torch.cuda.synchronize()
-        gather_ms = (time.perf_counter() - g0) * 1e3
+        dist.barrier()
+        g0 = time.perf_counter()
+        full = dist.gather_to_rank0(loc, total_videos)
+        torch.cuda.synchronize()
+        gather_ms = dist.max_over_ranks((time.perf_counter() - g0) * 1e3, device=dev)
+        if rank == 0:
+            gather_bytes = full.numel() * full.element_size()
+            # rank 0's own block arrives unchanged
+            assert torch.equal(full[:nv], loc), "gather: rank 0 block differs"
         del full
 
     cpu = None
     maxdiff = None
-    n_cpu = w["cpu_default"] if a.cpu_sample is None else a.cpu_sample
     cpu_e2e = None
-    if rank == 0 and world == 1 and not a.no_cpu_baseline and n_cpu > 0:
-        with threadpool_limits(1):
-            c = w["cpu"](n_cpu)
-        maxdiff, cpu_e2e = c["diff"], c["e2e_value"]
-        cpu = dict(value=c["value"], unit="kp-ts/s", cores=1, kind="port",
-                   sample=f"{c['sample']}, {c['dt']:.1f} s")
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        cores = cpu_cores() if a.cpu_cores is None else a.cpu_cores
+        plan = w["cpu_plan"](cores)
+        tasks = plan["tasks"]
+        one = [tasks[i] for i in plan["one"]]
+        t_fit1, hot1, outs1 = cpu_one_core(one)
+        wts = plan.get("weights") or [1] * len(one)
+        t_hot1 = sum(wi * ti for wi, ti in zip(wts, hot1))
+        used = max(1, min(cores, len(tasks)))
+        wall, outs = cpu_all_cores(tasks, used)
+        diffs = [float(abs(outs[i] - g).max()) for i, g in plan["gpu"].items()]
+        diffs += [float(abs(outs1[j] - plan["gpu"][i]).max())
+                  for j, i in enumerate(plan["one"]) if i in plan["gpu"]]
+        maxdiff = max(diffs)
+        if plan.get("weights") is None:
+            cpu_e2e = plan["units_one"] / (t_fit1 + t_hot1)
+        cpu = dict(value=plan["units_all"] / wall, unit="kp-ts/s", cores=used, kind="port",
+                   value_1core=plan["units_one"] / t_hot1,
+                   sample=(plan["what"].format(n=len(tasks)) + f", {used} processes x 1 thread "
+                           f"(numpy oracle: ensemble + filtering_pass + smooth_backward + "
+                           f"projection; model fit untimed), {wall:.1f} s wall; 1-core figure "
+                           f"on {plan['what'].format(n=len(one))}, {t_hot1:.1f} s"),
+                   host_cpus=len(os.sched_getaffinity(0)))
 
     if rank == 0:
         value = units_total / elapsed_max * a.steps
@@ -529,8 +659,13 @@ def main():
         }
         if "extra" in w:
             line.update(w["extra"]())
+        if world > 1:
+            import torch.distributed as tdist
+            line["distributed"] = dict(world_size=tdist.get_world_size(),
+                                       backend=str(tdist.get_backend()))
         if gather_ms is not None:
             line["gather_ms"] = gather_ms
+            line["gather_bytes"] = gather_bytes
         print(json.dumps(line))
     dist.barrier()
 

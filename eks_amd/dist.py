@@ -79,6 +79,10 @@ def gather_to_rank0(local, total_rows: int):
     if not (dist.is_available() and dist.is_initialized()):
         return local
     rank, world = dist.get_rank(), dist.get_world_size()
+    if local.is_cuda and dist.get_backend() == "gloo":
+        # gloo gathers host tensors (the CPU tests and the 1-GPU rehearsal)
+        full = gather_to_rank0(local.cpu(), total_rows)
+        return None if full is None else full.to(local.device)
     sizes = [shard_range(total_rows, world, r) for r in range(world)]
     rows = [hi - lo for lo, hi in sizes]
     cap = max(rows)

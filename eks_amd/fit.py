@@ -115,54 +115,6 @@ def pupil_model(preds, state_transition_matrix):
                 offset=np.array([mx, my] * 4), mx=mx, my=my)
 
 
-# --------------------------------------------------------------------------
-# batched single-view fit on device tensors (B trajectories at once)
-# --------------------------------------------------------------------------
-def _np_percentile_linear(x_sorted, q):
-    """np.percentile(..., q) 'linear' on rows of an ascending-sorted (B, T)
-    tensor: virtual index (T-1) q/100 and numpy's _lerp."""
-    T = x_sorted.shape[1]
-    vi = (T - 1) * (q / 100.0)
-    lo = int(np.floor(vi))
-    hi = min(lo + 1, T - 1)
-    g = vi - lo
-    a = x_sorted[:, lo]
-    b = x_sorted[:, hi]
-    d = b - a
-    return b - d * (1 - g) if g >= 0.5 else a + d * g
-
-
-def singleview_model_batch(preds, ens_vars, smooth_param, quantile_keep):
-    """Batched singleview_model on (B, T, 2) float64 CUDA tensors (preds /
-    ensemble variances as returned by eks_ensemble).  Returns a dict of
-    (B, ...) tensors (m0, S0, A, Q, C, offset)."""
-    import torch
-    B, T, n = preds.shape
-    worst = ens_vars.max(dim=2).values
-    thr = _np_percentile_linear(torch.sort(worst, dim=1).values, quantile_keep)
-    keep = worst <= thr[:, None]                              # (B, T)
-    cnt = keep.sum(dim=1).to(preds.dtype)                     # (B,)
-    offset = (preds * keep[..., None]).sum(dim=1) / cnt[:, None]
-    z = (preds - offset[:, None, :]) * keep[..., None]
-    zm = z.sum(dim=1) / cnt[:, None]
-    S0 = torch.diag_embed((((preds - offset[:, None, :] - zm[:, None, :]) ** 2)
-                           * keep[..., None]).sum(dim=1) / cnt[:, None])
-    # successive differences between consecutive KEPT frames
-    idx = torch.arange(T, device=preds.device).expand(B, T)
-    last = torch.where(keep, idx, torch.full_like(idx, -1)).cummax(dim=1).values
-    prev = torch.cat([torch.full_like(last[:, :1], -1), last[:, :-1]], dim=1)
-    pair = keep & (prev >= 0)
-    prev_c = prev.clamp(min=0)
-    d = preds - torch.gather(preds, 1, prev_c[..., None].expand(B, T, n))
-    npair = pair.sum(dim=1).to(preds.dtype)
-    dm = (d * pair[..., None]).sum(dim=1) / npair[:, None]
-    dc = (d - dm[:, None, :]) * pair[..., None]
-    Q = smooth_param * torch.einsum('bti,btj->bij', dc, dc) / (npair - 1)[:, None, None]
-    eye = torch.eye(n, dtype=preds.dtype, device=preds.device).expand(B, n, n)
-    return dict(m0=torch.zeros(B, n, dtype=preds.dtype, device=preds.device), S0=S0,
-                A=eye.clone(), Q=Q, C=eye.clone(), offset=offset)
-
-
 def paw_async_models(cam_preds, cam_vars, smooth_param, quantile_keep):
     """Model fit of the asynchronous paw smoother
     (eks/multiview_pca_smoother.py:124-241).  cam_preds / cam_vars: (2, T, 4)

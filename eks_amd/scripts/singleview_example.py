@@ -13,7 +13,7 @@ videos), scorer 'ensemble-kalman_tracker', likelihood 1.0.
 
 All (video, body part) trajectories with the same frame count and member
 count are smoothed in one batched GPU pass: ensemble (eks_ensemble), model
-fit on the device (eks_amd.fit.singleview_model_batch), fused smoother
+fit on the device (eks_amd.batch.fit -> eks_fit), fused smoother
 (eks_smooth with the A = C = I kernels).
 """
 from __future__ import annotations
@@ -45,9 +45,8 @@ def build_parser():
 def run(args):
     import torch
 
-    from eks_amd import _lib, batch, fit, io
+    from eks_amd import _lib, batch, io
     from eks_amd.scripts._common import resolve_save_dir
-    from eks_amd.smoothers import ensemble_stacks
     from eks_amd.utils import TRACKER
 
     _lib.require_gpu()
@@ -64,10 +63,11 @@ def run(args):
     files = []
     for (E, T, _), members in groups.items():
         stacks = np.concatenate([videos[i]["stack"] for i in members])  # (B, E, T, 2)
-        d, preds, ev = ensemble_stacks(stacks, args.ensembling_mode)
-        m = fit.singleview_model_batch(preds, ev, args.s, args.quantile_keep_pca)
-        params = batch.pack_params(m["m0"], m["S0"], m["A"], m["Q"], m["C"], m["offset"])
-        res = batch.smooth(d.permute(0, 2, 1, 3), params, n=2, r=2, mode=args.ensembling_mode,
+        d = torch.from_numpy(np.ascontiguousarray(stacks, dtype=np.float64)).to("cuda")
+        obs = d.permute(0, 2, 1, 3)                                      # (B, T, E, 2) view
+        params, _ = batch.fit(obs, kind="singleview", n=2, r=2, smooth_param=args.s,
+                              quantile_keep=args.quantile_keep_pca, mode=args.ensembling_mode)
+        res = batch.smooth(obs, params, n=2, r=2, mode=args.ensembling_mode,
                            flags=_lib.EKS_MODEL_A_IDENTITY | _lib.EKS_MODEL_C_IDENTITY,
                            check=True)
         out = res["out"].cpu().numpy()

@@ -8,7 +8,7 @@ runs the chunked scan of eks_smooth on its own frames, and the ranks exchange
 two small per-trajectory aggregates (the segment's filtering element, then its
 smoothing map: ~100 doubles per trajectory) with ``all_gather``.  The
 reference has no such path (its smoother is one sequential loop,
-eks/core.py:220-352); the results equal ``batch.smooth``'s to rounding.
+eks/ensemble_kalman.py:59-164); the results equal ``batch.smooth``'s to rounding.
 
     phase 1  K1 + segment element        -> all_gather -> combine(kind 0)
     phase 2  K2 + K3 (from the state)    -> all_gather -> combine(kind 1)

@@ -192,7 +192,7 @@ int eks_smooth_algo(int64_t B, int64_t T, int n, int r, int E, int algo);
  * rank k, and the chunked scan of eks_smooth runs per segment in three
  * phases with two exchanges of per-trajectory aggregates between them (the
  * reference has no equivalent: its smoother is one sequential loop,
- * eks/core.py:220-352).  Per segment of T frames starting at t_base of
+ * eks/ensemble_kalman.py:59-164).  Per segment of T frames starting at t_base of
  * T_total, with the arguments of eks_smooth (obs/out point at the segment's
  * own frames):
  *   phase 1: seg_out (B, EL), EL = R*R + 2R + R(R+1) <- the segment's aggregate

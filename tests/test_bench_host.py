@@ -1,0 +1,68 @@
+"""Host logic of bench.py that needs no GPU: the all-core CPU baseline
+(one spawned process per core, numpy oracle, BLAS single-threaded) gives
+the same outputs as the in-process 1-core run, tasks in order; the N-rank
+self-launch builds a torch.distributed.run command."""
+import os
+import sys
+
+import numpy as np
+
+import bench
+from eks_amd import synthetic
+
+
+def _tasks(n, T=400):
+    st = synthetic.singleview_obs(np.random.default_rng(7), 5, T, K=n).astype(np.float64)
+    return [("singleview", np.ascontiguousarray(st[:, :, k, :]), (0.01, 25.0)) for k in range(n)]
+
+
+def test_cpu_all_cores_matches_one_core():
+    tasks = _tasks(5)
+    before = os.environ.get("OPENBLAS_NUM_THREADS")
+    _, hot, outs1 = bench.cpu_one_core(tasks)
+    assert len(hot) == 5 and all(h > 0 for h in hot)
+    wall, outs = bench.cpu_all_cores(tasks, 2)
+    assert wall > 0
+    for a, b in zip(outs1, outs):
+        assert a.shape == (400, 2)
+        np.testing.assert_array_equal(a, b)
+    # the environment of this process is restored
+    assert os.environ.get("OPENBLAS_NUM_THREADS") == before
+
+
+def test_cpu_nll_task_is_oracle_nll():
+    from oracle import eks_oracle as O
+    t = _tasks(1)[0]
+    preds, ev = O.ensemble_array(t[1])
+    p = O.singleview_params(preds, ev, 0.01, 25.0)
+    task = ("nll", t[1], p)
+    _, _, outs = bench.cpu_one_core([task])
+    ref = O.compute_nll(preds - p["means"], p["m0"], p["S0"], p["C"], p["A"], p["Q"], ev)
+    assert outs[0] == ref
+
+
+def test_cpu_cores_respects_cap(monkeypatch):
+    monkeypatch.setenv("EKS_CPU_CORES", "1")
+    assert bench.cpu_cores() == 1
+    monkeypatch.delenv("EKS_CPU_CORES")
+    monkeypatch.setenv("OMP_NUM_THREADS", "3")
+    assert bench.cpu_cores() == min(3, len(os.sched_getaffinity(0)))
+
+
+def test_launch_ranks_command(monkeypatch):
+    seen = {}
+
+    def fake_call(cmd, env):
+        seen["cmd"], seen["env"] = cmd, env
+        return 0
+
+    import subprocess
+    monkeypatch.setattr(subprocess, "call", fake_call)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "4", "--steps", "3"])
+    a = bench.parse()
+    assert bench.launch_ranks(a) == 0
+    cmd = seen["cmd"]
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    assert "--nproc-per-node=4" in cmd and "127.0.0.1" in cmd
+    assert cmd[-4:] == ["--gpus", "4", "--steps", "3"]
+    assert seen["env"]["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"

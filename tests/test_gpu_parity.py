@@ -8,6 +8,7 @@ max|d| < 1e-5 (BASELINE.json) and in practice agree to ~1e-10.
 """
 import glob
 import os
+import warnings
 
 import numpy as np
 import pandas as pd
@@ -541,8 +542,7 @@ def _unpack(p, n, r):
 
 
 @pytest.mark.parametrize("E,T,q,dtype", [(5, 3000, 25, "f32"), (3, 257, 10, "f64"),
-                                         (4, 2000, 50, "f32"), (5, 1001, 100, "f64"),
-                                         (7, 500, 0, "f64")])
+                                         (4, 2000, 50, "f32"), (5, 1001, 100, "f64")])
 def test_fit_singleview_vs_host(torch, E, T, q, dtype):
     from eks_amd import batch, fit, synthetic
     from eks_amd.core import ensemble_array
@@ -560,6 +560,37 @@ def test_fit_singleview_vs_host(torch, E, T, q, dtype):
         got = _unpack(params[b], 2, 2)
         for k in ("m0", "S0", "A", "Q", "C", "offset"):
             _close(got[k], ref[k], rtol=1e-9)
+
+
+def test_fit_singleview_one_kept_frame(torch):
+    """q = 0 keeps exactly one frame (the minimum of the worst variance):
+    offset = that frame's ensemble average, S0 = 0 (variance of one point)
+    and Q = s * np.cov of zero consecutive-kept-frame differences, which
+    numpy defines as NaN (ddof 1 with no pairs; the reference's np.cov at
+    eks/multiview_pca_smoother.py:726-728 does the same).  The device fit
+    must give exactly that, with status 0 (a kept frame exists)."""
+    from eks_amd import batch, fit, synthetic
+    from eks_amd.core import ensemble_array
+    rng = np.random.default_rng(3500)
+    E, T, B = 7, 500, 6
+    st = np.stack([synthetic.singleview_obs(rng, E, T)[:, :, 0] for _ in range(B)]).astype(np.float64)
+    obs = torch.from_numpy(np.ascontiguousarray(st)).cuda().permute(0, 2, 1, 3)
+    params, status = batch.fit(obs, kind="singleview", n=2, r=2, smooth_param=0.01,
+                               quantile_keep=0, check=False)
+    assert (status.cpu().numpy() == 0).all()
+    params = params.cpu().numpy()
+    for b in range(B):
+        preds, ev = ensemble_array(st[b])
+        keep = np.argmin(ev.max(axis=1))
+        got = _unpack(params[b], 2, 2)
+        np.testing.assert_array_equal(got["offset"], preds[keep])
+        np.testing.assert_array_equal(got["S0"], np.zeros((2, 2)))
+        assert np.isnan(got["Q"]).all(), got["Q"]
+        with np.errstate(all="ignore"), warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            ref = fit.singleview_model(preds, ev, 0.01, 0)
+        assert np.isnan(ref["Q"]).all()
+        np.testing.assert_array_equal(ref["offset"], got["offset"])
 
 
 @pytest.mark.parametrize("V,T", [(2, 2000), (4, 1500), (3, 700)])

@@ -9,7 +9,8 @@ CSVs (separate passes), keeps the EKS kernels, and writes
   profiles/<tag>/summary.json          per-kernel average duration and HBM
                                        bytes per launch (FETCH_SIZE x 2 on
                                        gfx950 + WRITE_SIZE, both in KiB)
-and, if a workload key is given, profiles/pmc_latest.json for bench.py.
+and, if a workload key is given, bench_pmc.json at the repository root for
+bench.py (outside profiles/, which does not travel to the GPU box).
 """
 from __future__ import annotations
 
@@ -75,8 +76,8 @@ def main(src: str, dst: str, key: str | None = None):
     if key:
         pm = {"workload_key": key, "hbm_bytes_per_launch": tot_bytes,
               "source": os.path.join(dst, "summary.json"), "kernels": summary["kernels"]}
-        json.dump(pm, open(os.path.join(os.path.dirname(dst.rstrip("/")), "pmc_latest.json"), "w"),
-                  indent=1)
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        json.dump(pm, open(os.path.join(root, "bench_pmc.json"), "w"), indent=1)
     print(json.dumps(summary["per_call"]))
     for k, d in summary["kernels"].items():
         print(f"  {k:40s} {d.get('avg_ms', 0):8.3f} ms  {d['hbm_bytes'] / 1e9:7.3f} GB  "
