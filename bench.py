@@ -146,8 +146,9 @@ def _cpu_model(O, task):
     if kind == "nll":           # the model is given (a sweep candidate)
         return args
     preds, ev = O.ensemble_array(stack)
-    fit = {"singleview": O.singleview_params, "multicam": O.multicam_params,
-           "pupil": O.pupil_params}[kind]
+    if kind == "pupil":         # eks/pupil_smoother.py:109-172 (no variances)
+        return O.pupil_params(preds, *args)
+    fit = {"singleview": O.singleview_params, "multicam": O.multicam_params}[kind]
     return fit(preds, ev, *args)
 
 

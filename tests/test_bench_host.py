@@ -66,3 +66,19 @@ def test_launch_ranks_command(monkeypatch):
     assert "--nproc-per-node=4" in cmd and "127.0.0.1" in cmd
     assert cmd[-4:] == ["--gpus", "4", "--steps", "3"]
     assert seen["env"]["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+
+
+def test_cpu_task_kinds_match_oracle_smoothers():
+    """Each task kind's untimed fit + timed hot path equals the oracle's
+    whole-path function for that kind."""
+    from oracle import eks_oracle as O
+    rng = np.random.default_rng(11)
+    st_p = synthetic.pupil_obs(rng, 5, 300).astype(np.float64)               # (E, T, 8)
+    A = np.diag([0.99, 0.98, 0.98])
+    st_m = synthetic.multiview_obs(rng, 3, 5, 300, K=1)[:, :, 0].astype(np.float64)  # (E, T, 6)
+    tasks = [("pupil", st_p, (A,)), ("multicam", st_m, (0.01, 25.0)), _tasks(1)[0]]
+    _, _, outs = bench.cpu_one_core(tasks)
+    np.testing.assert_array_equal(outs[0], O.pupil_smooth(st_p, A)[0])
+    cams = [st_m[:, :, 2 * c:2 * c + 2] for c in range(3)]
+    np.testing.assert_allclose(outs[1], O.multicam_smooth(cams, 0.01, 25.0)[0], rtol=0, atol=1e-9)
+    np.testing.assert_array_equal(outs[2], O.singleview_smooth(tasks[2][1], 0.01, 25.0)[0])
