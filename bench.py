@@ -614,7 +614,7 @@ def main():
             one_desc = plan["what"].format(n=len(one))
         cpu = dict(value=plan["units_all"] / wall, unit="kp-ts/s", cores=used, kind="port",
                    value_1core=plan["units_one"] / t_hot1,
-                   sample=(plan["what"].format(n=len(tasks)) + f", {used} processes x 1 thread "
+                   sample=(plan["what"].format(n=len(tasks) - (1 if plan.get("weights") else 0)) + f", {used} processes x 1 thread "
                            f"(numpy oracle: ensemble + filtering_pass + smooth_backward + "
                            f"projection; model fit untimed), {wall:.1f} s wall; 1-core figure "
                            f"on {one_desc}, {t_hot1:.1f} s"),

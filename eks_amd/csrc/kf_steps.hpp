@@ -427,10 +427,16 @@ struct Elem {
 
 // Absorb one time step (predict with A, Q; update with the N scalar
 // observations of y, rv) into the running element.
+// With `acc`, the step's terms of the element's likelihood constant are
+// accumulated too: conditioned on x_{s-1} each scalar observation is
+// y_i ~ N(hb_i + g_i x_{s-1}, s_i), so
+//   -log p(y_{s..e-1} | x) = K + 1/2 x^T Jb x - eta^T x,
+//   K = 1/2 sum_i (log 2 pi + log s_i + e0_i^2 / s_i)   (acc.value)
+// which elem_nll_share turns into the chunk's NLL share.
 template <int R, int N, bool AI, bool CI>
 EKS_DEV void elem_absorb(Elem<R> &E, const double (&A)[R][R], const double (&Q)[R][R],
                          const double (&C)[N][R], const double (&y)[N], const double (&rv)[N],
-                         bool &ok) {
+                         bool &ok, NllAcc *acc = nullptr) {
   if constexpr (AI) {
 #pragma unroll
     for (int i = 0; i < R; ++i)
@@ -499,6 +505,7 @@ EKS_DEV void elem_absorb(Elem<R> &E, const double (&A)[R][R], const double (&Q)[
     const double inv = rcp_nr(s);
     const double e0 = y[i] - hb;
     const double ei = e0 * inv;
+    if (acc) acc->add(e0, s, inv);
 #pragma unroll
     for (int a = 0; a < R; ++a) {
       const double ga = g[a] * inv;
@@ -521,6 +528,55 @@ EKS_DEV void elem_absorb(Elem<R> &E, const double (&A)[R][R], const double (&Q)[
         if (c != a) E.Cb[c][a] = E.Cb[a][c];
       }
     }
+  }
+  if (acc) acc->renorm();
+}
+
+// determinant of a small matrix (adjugate for R <= 3, pivoted elimination above)
+template <int R>
+EKS_DEV double small_det(const double (&S)[R][R]) {
+  if constexpr (R == 1) {
+    return S[0][0];
+  } else if constexpr (R == 2) {
+    return fma(S[0][0], S[1][1], -S[0][1] * S[1][0]);
+  } else if constexpr (R == 3) {
+    const double c00 = fma(S[1][1], S[2][2], -S[1][2] * S[2][1]);
+    const double c01 = fma(S[1][2], S[2][0], -S[1][0] * S[2][2]);
+    const double c02 = fma(S[1][0], S[2][1], -S[1][1] * S[2][0]);
+    return fma(S[0][0], c00, fma(S[0][1], c01, S[0][2] * c02));
+  } else {
+    double a[R][R];
+    double det = 1.0;
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+#pragma unroll
+      for (int j = 0; j < R; ++j) a[i][j] = S[i][j];
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      int p = k;
+#pragma unroll
+      for (int i = k + 1; i < R; ++i)
+        if (fabs(a[i][k]) > fabs(a[p][k])) p = i;
+      if (p != k) {
+        det = -det;
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+          const double t = a[k][j];
+          a[k][j] = a[p][j];
+          a[p][j] = t;
+        }
+      }
+      det *= a[k][k];
+      if (a[k][k] == 0.0) return 0.0;
+      const double inv = 1.0 / a[k][k];
+#pragma unroll
+      for (int i = k + 1; i < R; ++i) {
+        const double f = a[i][k] * inv;
+#pragma unroll
+        for (int j = k + 1; j < R; ++j) a[i][j] = fma(-f, a[k][j], a[i][j]);
+      }
+    }
+    return det;
   }
 }
 
@@ -573,6 +629,58 @@ EKS_DEV bool compose_state(double (&m)[R], double (&P)[R][R], const Elem<R> &E) 
 #pragma unroll
     for (int j = 0; j < R; ++j) P[i][j] = 0.5 * (Pn[i][j] + Pn[j][i]);
   return ok;
+}
+
+// NLL share of the chunk [s, e) summarised by element E, given the filtered
+// x_{s-1} ~ N(m, P) (eks/ensemble_kalman.py:94-105's innovations, summed over
+// the chunk):
+//   -log E_x[exp(-K - 1/2 x^T Jb x + eta^T x)]
+//     = K - eta^T m + 1/2 m^T Jb m - 1/2 h^T (I + P Jb)^-1 P h + 1/2 log det(I + P Jb),
+//   h = eta - Jb m,
+// K = `kconst` (elem_absorb's accumulator).  Equal to the sum of the per-step
+// innovation terms of the sequential filter over the chunk (the algebra of
+// the Gaussian integral), without re-running that filter.
+template <int R>
+EKS_DEV double elem_nll_share(const double (&m)[R], const double (&P)[R][R], const Elem<R> &E,
+                              double kconst, bool &ok) {
+  double W[R][R], Mi[R][R], h[R], Ph[R];
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    double t = E.eta[i];
+#pragma unroll
+    for (int k = 0; k < R; ++k) t = fma(-E.Jb[i][k], m[k], t);
+    h[i] = t;
+  }
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    double t = 0.0;
+#pragma unroll
+    for (int k = 0; k < R; ++k) t = fma(P[i][k], h[k], t);
+    Ph[i] = t;
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      double w = (i == j) ? 1.0 : 0.0;
+#pragma unroll
+      for (int k = 0; k < R; ++k) w = fma(P[i][k], E.Jb[k][j], w);
+      W[i][j] = w;
+    }
+  }
+  const double det = small_det<R>(W);
+  ok = small_inverse<R>(W, Mi) && ok && det > 0.0;
+  double quad = 0.0, lin = 0.0, jm = 0.0;
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    double u = 0.0, jmi = 0.0;
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      u = fma(Mi[i][k], Ph[k], u);
+      jmi = fma(E.Jb[i][k], m[k], jmi);
+    }
+    quad = fma(h[i], u, quad);
+    lin = fma(E.eta[i], m[i], lin);
+    jm = fma(m[i], jmi, jm);
+  }
+  return kconst - lin + 0.5 * jm - 0.5 * quad + 0.5 * log(det);
 }
 
 // compose_state plus the chunk-level RTS map across the chunk.  With the

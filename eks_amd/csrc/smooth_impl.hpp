@@ -155,6 +155,11 @@ struct ChunkPlan {
   long long L = 0, NC = 0, NSUB = 0;
   int LS = 8;
   int smooth = 1;  // 0: filter only (out == NULL): NLL, no backward pass
+  // filter-only call of the whole pipeline: each chunk's NLL share is taken in
+  // closed form from its element (K1 stores the element's likelihood
+  // constant, K2 adds the start-state terms: elem_nll_share), so K3 does not
+  // re-run the filter
+  int nll_closed = 0;
   // members shared by all trajectories (batch stride 0, e.g. candidate models
   // of one trajectory): y / ev are stored once, as a single plane column
   long long yB = 0;
@@ -490,8 +495,8 @@ EKS_DEV void c1_stream(const SmoothArgs &a, const ChunkPlan &p, long long s, lon
       if (s + q < e)
 #pragma unroll
         for (int j = 0; j < N; ++j) {
-          yr[q][j] = pl((const YT *)p.ysrc, (s + q) * N + j, B, b);
-          er[q][j] = pl((const double *)p.evsrc, (s + q) * N + j, B, b);
+          yr[q][j] = pl((const YT *)p.ysrc, (s + q) * N + j, p.yB, p.ylane(b));
+          er[q][j] = pl((const double *)p.evsrc, (s + q) * N + j, p.yB, p.ylane(b));
         }
     for (long long t0 = s; t0 < e; t0 += DY) {
 #pragma unroll
@@ -507,8 +512,8 @@ EKS_DEV void c1_stream(const SmoothArgs &a, const ChunkPlan &p, long long s, lon
           if (t + DY < e)
 #pragma unroll
             for (int j = 0; j < N; ++j) {
-              yr[q][j] = pl((const YT *)p.ysrc, (t + DY) * N + j, B, b);
-              er[q][j] = pl((const double *)p.evsrc, (t + DY) * N + j, B, b);
+              yr[q][j] = pl((const YT *)p.ysrc, (t + DY) * N + j, p.yB, p.ylane(b));
+              er[q][j] = pl((const double *)p.evsrc, (t + DY) * N + j, p.yB, p.ylane(b));
             }
           absorb(t, y, rv);
         }
@@ -558,6 +563,30 @@ EKS_DEV void c1_stream(const SmoothArgs &a, const ChunkPlan &p, long long s, lon
   }
 }
 
+// Members shared by every trajectory (batch stride 0: candidate models of one
+// recording, the pupil NLL sweep): the ensemble of each step is computed ONCE
+// here, one lane per step, into the single-column y / ev planes (yB = 1) that
+// K1 (as YevIn input), K3 and K5 then read for every trajectory, instead of
+// every (chunk, trajectory) lane re-reducing the same members.
+template <int E, int N, typename T, typename YT>
+__global__ __launch_bounds__(kBlock) void k_c0_shared(SmoothArgs a, ChunkPlan p) {
+  const long long t = blockIdx.x * (long long)kBlock + threadIdx.x;
+  if (t >= a.T) return;
+  constexpr int EE = E > 0 ? E : 1;
+  const T *pt = (const T *)a.obs + t * a.st;
+  T cur[EE][N];
+  if constexpr (E > 0) load_step<E, N, T>(pt, a.se, a.sj, cur);
+  double avg[N], rv[N];
+  reduce_step<E, N, T>(cur, pt, a.se, a.sj, a.E, a.median != 0, avg, rv);
+  YT *ybuf = (YT *)(a.ws + p.y_off);
+  double *evbuf = (double *)(a.ws + p.ev_off);
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    ybuf[t * N + j] = (YT)avg[j];
+    evbuf[t * N + j] = rv[j];
+  }
+}
+
 template <int R, int N, int E, typename T, typename YT, bool AI, bool CI, bool UNI>
 __global__ __launch_bounds__(kBlock) void k_c1_elem(SmoothArgs a, ChunkPlan p) {
   constexpr int D = (E > 0 && E * N <= 16) ? 2 : 1;  // member prefetch distance (steps)
@@ -589,6 +618,7 @@ __global__ __launch_bounds__(kBlock) void k_c1_elem(SmoothArgs a, ChunkPlan p) {
       if (t > 0) kf_predict<R, AI>(m, P, md.A, md.Q);
       kf_update<R, N, CI>(m, P, md.C, y, rv, acc, ok);
     });
+    if (p.nll_closed) pl((double *)(a.ws + p.nllp_off), c, B, b) = acc.value((double)(e - s) * N);
     El.set_identity();
 #pragma unroll
     for (int i = 0; i < R; ++i) {
@@ -601,10 +631,12 @@ __global__ __launch_bounds__(kBlock) void k_c1_elem(SmoothArgs a, ChunkPlan p) {
     }
   } else {
     El.set_identity();
+    NllAcc acc;
     c1_stream<E, N, T, YT, D>(a, p, s, e, b, md.off, [&](long long, const double (&y)[N],
                                                           const double (&rv)[N]) {
-      elem_absorb<R, N, AI, CI>(El, md.A, md.Q, md.C, y, rv, ok);
+      elem_absorb<R, N, AI, CI>(El, md.A, md.Q, md.C, y, rv, ok, &acc);
     });
+    if (p.nll_closed) pl((double *)(a.ws + p.nllp_off), c, B, b) = acc.value((double)(e - s) * N);
   }
   El.store((double *)(a.ws + p.elem_off) + ((long long)b * p.NC + c) * Elem<R>::len, 1);
   if (!ok) flag(a.status, b, first ? EKS_STATUS_SINGULAR : EKS_STATUS_SCAN);
@@ -646,11 +678,14 @@ __global__ __launch_bounds__(64) void k_c2_fscan(SmoothArgs a, ChunkPlan p) {
   }
   // software pipelined: the element of chunk c+1 is in flight while chunk c
   // is composed (the chain is latency bound, not bandwidth bound)
+  double *np_ = (double *)(a.ws + p.nllp_off);
+  const bool nllc = p.nll_closed && a.t_base == 0;
   if (p.NC > 1) El.load(erow + Elem<R>::len, 1);
   for (long long c = 1; c < p.NC; ++c) {
     store_state<R>(cst + (c * KS) * B + b, B, m, P);
+    if (c + 1 < p.NC && (nllc || c + 2 < p.NC)) Nx.load(erow + (c + 1) * Elem<R>::len, 1);
+    if (nllc) np_[c * B + b] = elem_nll_share<R>(m, P, El, np_[c * B + b], ok);
     if (c + 1 < p.NC) {
-      if (c + 2 < p.NC) Nx.load(erow + (c + 1) * Elem<R>::len, 1);
       ok = compose_state<R>(m, P, El) && ok;
       El = Nx;
     }
@@ -758,12 +793,14 @@ __global__ __launch_bounds__(64 * W) void k_c2_fscan_w(SmoothArgs a, ChunkPlan p
         for (int j = 0; j < R; ++j) P[i][j] = ex.Cb[i][j];
       }
     }
+    double *np_ = (double *)(a.ws + p.nllp_off);
     for (; c < c1; ++c) {
       store_state<R>(cst + (c * KS) * B + b, B, m, P);
-      if (c + 1 < c1) {
+      if (c + 1 < c1 || p.nll_closed) {
         Elem<R> e;
         e.load(elem + (b * NC + c) * Elem<R>::len, 1);
-        ok = compose_state<R>(m, P, e) && ok;
+        if (p.nll_closed) np_[c * B + b] = elem_nll_share<R>(m, P, e, np_[c * B + b], ok);
+        if (c + 1 < c1) ok = compose_state<R>(m, P, e) && ok;
       }
     }
   }
@@ -1376,7 +1413,9 @@ int launch_shape(const SmoothArgs &a, int algo, long long L) {
   }
   ChunkPlan p = make_plan(a.B, a.T, R, N, L);
   p.smooth = a.out != nullptr;
-  p.yB = (!yev && a.sb == 0 && a.B > 1) ? 1 : a.B;
+  p.nll_closed = (!p.smooth && a.phase == 0 && a.nll) ? 1 : 0;
+  const bool shared = !yev && a.sb == 0 && a.B > 1;
+  p.yB = shared ? 1 : a.B;
   const bool uni = uniform_lanes(a.B);
   const unsigned gch = uni ? (unsigned)(p.NC * blocks_per_chunk(a.B))
                            : grid_for(p.NC * a.B, kBlock);
@@ -1390,13 +1429,14 @@ int launch_shape(const SmoothArgs &a, int algo, long long L) {
     p.ysrc = a.ws + p.y_off;
     p.evsrc = a.ws + p.ev_off;
   }
+  bool begun = false;  // the profiler's call already opened (k_c0_shared)
   auto run = [&](auto tag, auto ytag, auto unitag) -> int {
     using Tp = decltype(tag);
     using YT = decltype(ytag);
     constexpr bool U = decltype(unitag)::value;
     constexpr int LS = sub_len_c(R, N);
     const int ph = a.phase;  // 0: whole pipeline; 1 / 2 / 3: time-segment phases
-    prof_call_begin();
+    if (!begun) prof_call_begin();
     int rc;
     if (ph == 0 || ph == 1) {
       auto k1 = [&](auto Ec) {
@@ -1445,10 +1485,12 @@ int launch_shape(const SmoothArgs &a, int algo, long long L) {
         hipLaunchKernelGGL((k_c2_fscan_w<R, N, 1>), dim3((unsigned)a.B), dim3(64), 0, a.stream,
                            a, p);
       if ((rc = check_launch("k_c2_fscan"))) return rc;
-      prof_mark(a.stream, "k_c3_rerun");
-      hipLaunchKernelGGL((k_c3_rerun<R, N, YT, AI, CI, LS, U>), dim3(gch), dim3(kBlock), 0,
-                         a.stream, a, p);
-      if ((rc = check_launch("k_c3_rerun"))) return rc;
+      if (!p.nll_closed) {
+        prof_mark(a.stream, "k_c3_rerun");
+        hipLaunchKernelGGL((k_c3_rerun<R, N, YT, AI, CI, LS, U>), dim3(gch), dim3(kBlock), 0,
+                           a.stream, a, p);
+        if ((rc = check_launch("k_c3_rerun"))) return rc;
+      }
       if (ph == 2 && p.smooth) {  // the segment's aggregate RTS map
         prof_mark(a.stream, "k_seg_maps");
         if (sw == 8)
@@ -1490,6 +1532,27 @@ int launch_shape(const SmoothArgs &a, int algo, long long L) {
     return uni ? run(tag, ytag, std::true_type{}) : run(tag, ytag, std::false_type{});
   };
   if (yev) return y32 ? with_uni(YevIn<float>{}, float{}) : with_uni(YevIn<double>{}, double{});
+  if (shared) {
+    // the ensemble once (k_c0_shared), then the pipeline on those planes
+    if (a.phase == 0 || a.phase == 1) {
+      auto k0 = [&](auto tag, auto ytag) -> int {
+        using Tp = decltype(tag);
+        using YT = decltype(ytag);
+        return dispatch_members_c(a.E, [&](auto Ec) {
+          constexpr int EE = decltype(Ec)::value;
+          prof_mark(a.stream, "k_c0_shared");
+          hipLaunchKernelGGL((k_c0_shared<EE, N, Tp, YT>), dim3(grid_for(a.T, kBlock)),
+                             dim3(kBlock), 0, a.stream, a, p);
+          return check_launch("k_c0_shared");
+        });
+      };
+      prof_call_begin();
+      begun = true;
+      const int rc = y32 ? k0(float{}, float{}) : f32 ? k0(float{}, double{}) : k0(double{}, double{});
+      if (rc) return rc;
+    }
+    return y32 ? with_uni(YevIn<float>{}, float{}) : with_uni(YevIn<double>{}, double{});
+  }
   if (y32) return with_uni(float{}, float{});
   return f32 ? with_uni(float{}, double{}) : with_uni(double{}, double{});
 }

@@ -774,3 +774,40 @@ def test_algo3_coarse_subparts(torch, S, monkeypatch):
         assert float((got["out"] - ref["out"]).abs().max()) < 1e-8, T
         assert float((got["ms"] - ref["ms"]).abs().max()) < 1e-8, T
         torch.testing.assert_close(got["nll"], ref["nll"], rtol=1e-10, atol=0)
+
+
+@pytest.mark.parametrize("kind,B,T", [("singleview", 1, 100), ("singleview", 5, 3000),
+                                      ("singleview", 300, 5000), ("singleview", 17, 30000),
+                                      ("multicam", 3, 20000), ("multicam", 40, 2000)])
+def test_filter_only_closed_form_nll(torch, kind, B, T):
+    """Filter-only calls take each chunk's NLL share in closed form from its
+    filtering element and the chunk's start state (kf_steps.hpp
+    elem_nll_share) instead of re-running the filter: it must equal the
+    sequential filter's NLL (algo 1) to rtol 1e-10, for short (sequential
+    K2) and long (wave-parallel K2) chunk chains, own and shared members."""
+    from eks_amd import _lib, batch, synthetic
+    rng = np.random.default_rng(B * 7 + T)
+    if kind == "singleview":
+        st = synthetic.singleview_obs(rng, 5, T, K=B).transpose(2, 0, 1, 3)   # (B, E, T, 2)
+        n, r, flags = 2, 2, _lib.EKS_MODEL_A_IDENTITY | _lib.EKS_MODEL_C_IDENTITY
+    else:
+        st = synthetic.multiview_obs(rng, 3, 5, T, K=B).transpose(2, 0, 1, 3)  # (B, E, T, 6)
+        n, r, flags = 6, 3, _lib.EKS_MODEL_A_IDENTITY
+    obs = batch.make_time_major(st, dtype=np.float32)
+    params, _ = batch.fit(obs, kind=kind, n=n, r=r, smooth_param=0.01, quantile_keep=25)
+    ref = batch.smooth(obs, params, n=n, r=r, algo=1, flags=flags, want_nll=True)["nll"]
+    got = batch.nll(obs, params, n=n, r=r, algo=2, flags=flags)
+    rel = float(((got - ref) / ref.abs()).abs().max())
+    assert rel < 1e-10, rel
+    # one recording scored under B candidate models (members shared, stride 0)
+    one = obs[:1].expand(B, -1, -1, -1)
+    p1 = params[:1].expand(B, -1).contiguous()
+    p1[:, -n:] += torch.arange(B, dtype=torch.float64, device=p1.device)[:, None] * 0.25
+    ref1 = batch.smooth(one, p1, n=n, r=r, algo=1, flags=flags, want_nll=True)["nll"]
+    got1 = batch.nll(one, p1, n=n, r=r, algo=2, flags=flags)
+    rel1 = float(((got1 - ref1) / ref1.abs()).abs().max())
+    assert rel1 < 1e-10, rel1
+    # and smoothed under them (k_c0_shared: the shared ensemble computed once)
+    o2 = batch.smooth(one, p1, n=n, r=r, algo=2, flags=flags)["out"]
+    o1 = batch.smooth(one, p1, n=n, r=r, algo=1, flags=flags)["out"]
+    assert float((o2 - o1).abs().max()) < 1e-8
