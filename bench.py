@@ -70,6 +70,9 @@ def parse():
     ap.add_argument("--no-gather", action="store_true",
                     help="config 4, N > 1: skip the final gather of all outputs to rank 0 "
                          "(RCCL), timed once after the throughput loop")
+    ap.add_argument("--dense-pupil", action="store_true",
+                    help="config 5: run the pupil model through the dense r=3, n=8 kernels "
+                         "instead of the EKS_MODEL_PUPIL ones (comparison runs)")
     ap.add_argument("--timeshard", action="store_true",
                     help="config 5: split the frames over the ranks (eks_amd.timeshard: two "
                          "all_gathers of per-segment aggregates) instead of replicas")
@@ -376,6 +379,8 @@ def workload_pupil(torch, a, dev, rank, world):
     ms = torch.empty((1, T, 3), dtype=torch.float64, device=dev)
     status = torch.empty((1,), dtype=torch.int32, device=dev)
     cands_obs = obs.expand(len(cands), -1, -1, -1)  # batch stride 0: members shared
+    # pupil structure (C = pupil matrix, A / Q diagonal): EKS_MODEL_PUPIL kernels
+    flags = 0 if a.dense_pupil else batch.model_flags(stackp("A"), stackp("C"), stackp("Q"))
     state = {}
     t0, Tk = 0, T
     if a.timeshard:
@@ -385,20 +390,21 @@ def workload_pupil(torch, a, dev, rank, world):
 
     def step_timeshard():
         scores = timeshard.smooth_time_sharded(cands_obs[:, t0:t0 + Tk], params, n=8, r=3,
-                                               t_base=t0, T_total=T, want_out=False)["nll"]
+                                               t_base=t0, T_total=T, want_out=False,
+                                               flags=flags)["nll"]
         best = torch.argmin(scores)            # the same on every rank (summed NLL)
         p_best = params.index_select(0, best.view(1)).contiguous()
         r = timeshard.smooth_time_sharded(obs[:, t0:t0 + Tk], p_best, n=8, r=3, t_base=t0,
-                                          T_total=T, out=seg_out, want_ms=True)
+                                          T_total=T, out=seg_out, want_ms=True, flags=flags)
         state["best"], state["scores"], state["ms"] = best, scores, r["ms"]
         status.copy_(r["status"])
 
     def step():
-        scores = batch.nll(cands_obs, params, n=8, r=3, algo=a.algo, check=False)
+        scores = batch.nll(cands_obs, params, n=8, r=3, algo=a.algo, check=False, flags=flags)
         best = torch.argmin(scores)                                    # stays on device
         p_best = params.index_select(0, best.view(1)).contiguous()
         r = batch.smooth(obs, p_best, n=8, r=3, out=out, want_ms=True, status=status,
-                         algo=a.algo)
+                         algo=a.algo, flags=flags)
         state["best"], state["scores"], state["ms"] = best, scores, r["ms"]
 
     def cpu_plan(cores):

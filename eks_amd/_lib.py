@@ -18,7 +18,7 @@ HEADERS = [HEADER, os.path.join(os.path.dirname(HERE), "include", "eks_io.h")]
 
 EKS_OK, EKS_ERR_ARG, EKS_ERR_UNSUPPORTED, EKS_ERR_HIP = 0, 1, 2, 4
 EKS_STATUS_SINGULAR, EKS_STATUS_BAD_MODEL, EKS_STATUS_SCAN = 1, 2, 4
-EKS_MODEL_A_IDENTITY, EKS_MODEL_C_IDENTITY = 1, 2
+EKS_MODEL_A_IDENTITY, EKS_MODEL_C_IDENTITY, EKS_MODEL_PUPIL = 1, 2, 4
 EKS_FIT_SINGLEVIEW, EKS_FIT_MULTICAM = 1, 2
 EKS_F32, EKS_F64 = 0, 1
 EKS_YEV32, EKS_YEV64 = 2, 3

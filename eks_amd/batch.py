@@ -77,9 +77,20 @@ def workspace(nbytes: int, device=None, slot: str = "smooth"):
     return buf
 
 
-def model_flags(A, C) -> int:
+# the pupil measurement matrix (eks/pupil_smoother.py:150-153; fit.PUPIL_C)
+_PUPIL_C = np.array([[0, 1, 0], [-.5, 0, 1], [0, 1, 0], [.5, 0, 1],
+                     [.5, 1, 0], [0, 0, 1], [-.5, 1, 0], [0, 0, 1]], dtype=np.float64)
+
+
+def _diagonal(M) -> bool:
+    off = ~np.eye(M.shape[-1], dtype=bool)
+    return bool(np.all(M[..., off] == 0))
+
+
+def model_flags(A, C, Q=None) -> int:
     """EKS_MODEL_* promise bits for host-side model arrays (A (.., r, r),
-    C (.., n, r)): set when every trajectory's A (resp. C) is the identity."""
+    C (.., n, r), Q (.., r, r)): A / C identity for every trajectory, or
+    (with Q) the pupil structure -- C the pupil matrix, A and Q diagonal."""
     A = np.asarray(A)
     C = np.asarray(C)
     f = 0
@@ -87,6 +98,9 @@ def model_flags(A, C) -> int:
         f |= _lib.EKS_MODEL_A_IDENTITY
     if C.shape[-1] == C.shape[-2] and np.all(C == np.eye(C.shape[-1])):
         f |= _lib.EKS_MODEL_C_IDENTITY
+    if (Q is not None and C.shape[-2:] == (8, 3) and np.all(C == _PUPIL_C)
+            and _diagonal(A) and _diagonal(np.asarray(Q))):
+        f |= _lib.EKS_MODEL_PUPIL
     return f
 
 
@@ -155,7 +169,7 @@ def smooth(obs, params, *, n: int, r: int, mode: str = "median", out=None, want_
     if check:
         st_all = status_bits(status)
         if st_all & _lib.EKS_STATUS_BAD_MODEL:
-            raise ValueError("model_flags promise A = I / C = I does not hold")
+            raise ValueError("a model_flags promise (A = I / C = I / pupil structure) does not hold")
         if st_all & _lib.EKS_STATUS_SCAN and algo != 1:
             return smooth(obs, params, n=n, r=r, mode=mode, out=out, want_ms=want_ms,
                           want_nll=want_nll, status=status, algo=1, flags=flags,

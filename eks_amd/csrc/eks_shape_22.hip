@@ -7,8 +7,8 @@ namespace eks {
 int launch_22(const SmoothArgs &a, int algo, long long L) {
   const int flags = a.flags;
   if ((flags & EKS_MODEL_A_IDENTITY) && (flags & EKS_MODEL_C_IDENTITY))
-    return launch_shape<2, 2, true, true>(a, algo, L);
-  return launch_shape<2, 2, false, false>(a, algo, L);
+    return launch_shape<2, 2, kAId, kCId>(a, algo, L);
+  return launch_shape<2, 2, kAGen, kCGen>(a, algo, L);
 }
 
 }  // namespace eks

@@ -6,8 +6,8 @@ namespace eks {
 
 int launch_36(const SmoothArgs &a, int algo, long long L) {
   const int flags = a.flags;
-  if (flags & EKS_MODEL_A_IDENTITY) return launch_shape<3, 6, true, false>(a, algo, L);
-  return launch_shape<3, 6, false, false>(a, algo, L);
+  if (flags & EKS_MODEL_A_IDENTITY) return launch_shape<3, 6, kAId, kCGen>(a, algo, L);
+  return launch_shape<3, 6, kAGen, kCGen>(a, algo, L);
 }
 
 }  // namespace eks

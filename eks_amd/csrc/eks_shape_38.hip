@@ -6,8 +6,9 @@ namespace eks {
 
 int launch_38(const SmoothArgs &a, int algo, long long L) {
   const int flags = a.flags;
-  if (flags & EKS_MODEL_A_IDENTITY) return launch_shape<3, 8, true, false>(a, algo, L);
-  return launch_shape<3, 8, false, false>(a, algo, L);
+  if (flags & EKS_MODEL_PUPIL) return launch_shape<3, 8, kADiag, kCPupil>(a, algo, L);
+  if (flags & EKS_MODEL_A_IDENTITY) return launch_shape<3, 8, kAId, kCGen>(a, algo, L);
+  return launch_shape<3, 8, kAGen, kCGen>(a, algo, L);
 }
 
 }  // namespace eks

@@ -77,6 +77,8 @@ static int smooth_call(const void *obs, int obs_dtype, int64_t B, int64_t T, int
                    "eks_smooth: (r=%d, n=%d) not compiled in (have (2,2) (3,4) (3,6) (3,8))", r, n);
   if ((model_flags & EKS_MODEL_C_IDENTITY) && r != n)
     return set_err(EKS_ERR_ARG, "eks_smooth: C = I needs r == n");
+  if ((model_flags & EKS_MODEL_PUPIL) && (r != 3 || n != 8))
+    return set_err(EKS_ERR_ARG, "eks_smooth: EKS_MODEL_PUPIL needs r = 3, n = 8");
   if (B == 0) return EKS_OK;
   int al = phase ? 2 : pick_algo(B, T, n, r, E, algo);
   const size_t need = phase ? make_plan(B, T, r, n, chunk_len(B, T, r)).total

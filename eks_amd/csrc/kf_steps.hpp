@@ -2,16 +2,22 @@
 // sequential (eks_smooth.hip) and time-parallel (eks_chunked.hip) kernels.
 //
 // Conventions: R = latent dimension r, N = observation dimension n.
-// AI = "A is the identity" and CI = "C is the identity (R == N)" are
-// compile-time structure flags: the single-view model has A = C = I2
-//  and the multi-camera model A = I3
-// (eks/multiview_pca_smoother.py:724).  The host promises the structure and
-// the kernels verify it per trajectory (status bit EKS_STATUS_BAD_MODEL on violation).
+// AI / CI are compile-time model-structure kinds (EKS_MODEL_* promises):
+//   AI: kAGen, kAId (A = I: the single-view model, SURVEY.md §8 A6, and the
+//       multi-camera model, eks/multiview_pca_smoother.py:724) or kADiag (A
+//       and Q diagonal: the pupil model, eks/pupil_smoother.py:140-147);
+//   CI: kCGen, kCId (C = I, R == N: single view) or kCPupil (C = the pupil
+//       measurement matrix of eks/pupil_smoother.py:150-153, R = 3, N = 8).
+// The host promises the structure and the kernels verify it per trajectory
+// (status bit EKS_STATUS_BAD_MODEL on violation).
 #pragma once
 #include "eks_common.hpp"
 #include "small_linalg.hpp"
 
 namespace eks {
+
+constexpr int kAGen = 0, kAId = 1, kADiag = 2;
+constexpr int kCGen = 0, kCId = 1, kCPupil = 2;
 
 template <int R>
 struct Sym {
@@ -57,6 +63,29 @@ EKS_DEV bool is_identity_rect(const double (&M)[N][R]) {
   for (int i = 0; i < N; ++i)
 #pragma unroll
     for (int j = 0; j < R; ++j) ok = ok && (M[i][j] == (i == j ? 1.0 : 0.0));
+  return ok;
+}
+
+template <int R>
+EKS_DEV bool is_diagonal(const double (&M)[R][R]) {
+  bool ok = true;
+#pragma unroll
+  for (int i = 0; i < R; ++i)
+#pragma unroll
+    for (int j = 0; j < R; ++j) ok = ok && (i == j || M[i][j] == 0.0);
+  return ok;
+}
+
+// C equals the pupil measurement matrix (eks/pupil_smoother.py:150-153)
+template <int N, int R>
+EKS_DEV bool is_pupil_c(const double (&M)[N][R]) {
+  constexpr double P[8][3] = {{0, 1, 0}, {-.5, 0, 1}, {0, 1, 0}, {.5, 0, 1},
+                              {.5, 1, 0}, {0, 0, 1},  {-.5, 1, 0}, {0, 0, 1}};
+  bool ok = (N == 8 && R == 3);
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+#pragma unroll
+    for (int j = 0; j < R; ++j) ok = ok && (i < 8 && j < 3 && M[i][j] == P[i < 8 ? i : 0][j < 3 ? j : 0]);
   return ok;
 }
 
@@ -147,10 +176,10 @@ EKS_DEV void ensemble_col(const T (&raw)[E], bool median, double &avg, double &v
 // Kalman filter pieces
 // ---------------------------------------------------------------------------
 // prior of step t from the posterior of t-1:  m <- A m,  P <- A (P A^T) + Q
-template <int R, bool AI>
+template <int R, int AI>
 EKS_DEV void kf_predict(double (&m)[R], double (&P)[R][R], const double (&A)[R][R],
                         const double (&Q)[R][R]) {
-  if constexpr (AI) {
+  if constexpr (AI == kAId) {
 #pragma unroll
     for (int i = 0; i < R; ++i)
 #pragma unroll
@@ -158,6 +187,17 @@ EKS_DEV void kf_predict(double (&m)[R], double (&P)[R][R], const double (&A)[R][
         P[i][j] += Q[i][j];
         if (j != i) P[j][i] = P[i][j];
       }
+  } else if constexpr (AI == kADiag) {  // A, Q diagonal
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+#pragma unroll
+      for (int j = i; j < R; ++j) {
+        const double t = (A[i][i] * P[i][j]) * A[j][j];
+        P[i][j] = (i == j) ? t + Q[i][i] : t;
+        if (j != i) P[j][i] = P[i][j];
+      }
+      m[i] *= A[i][i];
+    }
   } else {
     double PAt[R][R], mp[R];
     matmul_nt<R, R, R>(P, A, PAt);
@@ -198,15 +238,96 @@ struct NllAcc {
   }
 };
 
+// ---------------------------------------------------------------------------
+// Pupil measurement rows (eks/pupil_smoother.py:150-153, PUPIL_KEYS order:
+// top x, y, bottom x, y, right x, y, left x, y; state (diameter, com_x,
+// com_y)), coefficients in half units.  Rows 0 / 2 ([0 1 0]) and 5 / 7
+// ([0 0 1]) are equal: each pair is folded into ONE scalar observation
+// (merge_obs), so a step is 6 sparse scalar updates instead of 8 dense ones.
+// ---------------------------------------------------------------------------
+// c . x for c = (H0, H1, H2) / 2, zero coefficients skipped: exact products
+// by 1 and 1/2, the same value as the dense fma chain over the row
+template <int H0, int H1, int H2>
+EKS_DEV double cdot3(double x0, double x1, double x2) {
+  constexpr double c0 = 0.5 * H0, c1 = 0.5 * H1, c2 = 0.5 * H2;
+  double s = 0.0;
+  if constexpr (H0 != 0) s = c0 * x0;
+  if constexpr (H1 != 0) {
+    if constexpr (H0 != 0) s = fma(c1, x1, s);
+    else s = c1 * x1;
+  }
+  if constexpr (H2 != 0) {
+    if constexpr (H0 != 0 || H1 != 0) s = fma(c2, x2, s);
+    else s = c2 * x2;
+  }
+  return s;
+}
+
+// Two scalar observations (y1, r1), (y2, r2) of the same row c: their joint
+// density is N(y; c x, r) N(y1 - y2; 0, r1 + r2) with
+//   y = (r2 y1 + r1 y2) / (r1 + r2),  r = r1 r2 / (r1 + r2),
+// i.e. one scalar observation plus a state-free NLL term (added to `acc`).
+// r1 + r2 = 0 (both exact) is the reference's singular S.
+EKS_DEV void merge_obs(double y1, double r1, double y2, double r2, double &y, double &r,
+                       NllAcc *acc, bool &ok) {
+  const double sr = r1 + r2;
+  ok = ok && !(sr <= 0.0);
+  const double inv = rcp_nr(sr);
+  y = fma(r2, y1, r1 * y2) * inv;
+  r = (r1 * r2) * inv;
+  if (acc) acc->add(y1 - y2, sr, inv);
+}
+
+// one scalar update of the filter state with pupil row H (kf_update's body)
+template <int H0, int H1, int H2>
+EKS_DEV void kf_update_row(double (&m)[3], double (&P)[3][3], double y, double rv, NllAcc &acc,
+                           bool &ok) {
+  double v[3];
+#pragma unroll
+  for (int a = 0; a < 3; ++a) v[a] = cdot3<H0, H1, H2>(P[a][0], P[a][1], P[a][2]);
+  const double s = rv + cdot3<H0, H1, H2>(v[0], v[1], v[2]);
+  const double hm = cdot3<H0, H1, H2>(m[0], m[1], m[2]);
+  ok = ok && !(s <= 0.0);
+  const double inv = rcp_nr(s);
+  const double e = y - hm;
+  acc.add(e, s, inv);
+  const double ei = e * inv;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) m[a] = fma(v[a], ei, m[a]);
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    const double ka = v[a] * inv;
+#pragma unroll
+    for (int c = a; c < 3; ++c) {
+      P[a][c] = fma(-ka, v[c], P[a][c]);
+      if (c != a) P[c][a] = P[a][c];
+    }
+  }
+}
+
 // Measurement update with diagonal R, one scalar observation at a time
 // (algebraically the reference's kalman_dot with the n x n solve).
-template <int R, int N, bool CI>
+template <int R, int N, int CI>
 EKS_DEV void kf_update(double (&m)[R], double (&P)[R][R], const double (&C)[N][R],
                        const double (&y)[N], const double (&rv)[N], NllAcc &acc, bool &ok) {
+  if constexpr (CI == kCPupil) {
+    static_assert(R == 3 && N == 8, "the pupil model is r = 3, n = 8");
+    double ya, ra, yb, rb;
+    merge_obs(y[0], rv[0], y[2], rv[2], ya, ra, &acc, ok);
+    merge_obs(y[5], rv[5], y[7], rv[7], yb, rb, &acc, ok);
+    kf_update_row<0, 2, 0>(m, P, ya, ra, acc, ok);
+    kf_update_row<-1, 0, 2>(m, P, y[1], rv[1], acc, ok);
+    kf_update_row<1, 0, 2>(m, P, y[3], rv[3], acc, ok);
+    kf_update_row<1, 2, 0>(m, P, y[4], rv[4], acc, ok);
+    kf_update_row<0, 0, 2>(m, P, yb, rb, acc, ok);
+    kf_update_row<-1, 2, 0>(m, P, y[6], rv[6], acc, ok);
+    acc.renorm();
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < N; ++i) {
     double v[R], s, hm;
-    if constexpr (CI) {
+    if constexpr (CI == kCId) {
 #pragma unroll
       for (int a = 0; a < R; ++a) v[a] = P[a][i];
       s = v[i] + rv[i];
@@ -296,17 +417,25 @@ EKS_DEV bool small_inverse(const double (&S)[R][R], double (&Si)[R][R]) {
 // RTS gain and offset at step t from the filtered (m, P):
 //   S = A P A^T + Q,  J = P A^T S^-1,  d = m - J A m
 // so that ms[t] = J ms[t+1] + d  (eks/ensemble_kalman.py:158, :161).
-template <int R, bool AI>
+template <int R, int AI>
 EKS_DEV bool rts_gain(const double (&m)[R], const double (&P)[R][R], const double (&A)[R][R],
                       const double (&Q)[R][R], double (&J)[R][R], double (&d)[R]) {
   double S[R][R], PAt[R][R], Si[R][R];
-  if constexpr (AI) {
+  if constexpr (AI == kAId) {
 #pragma unroll
     for (int i = 0; i < R; ++i)
 #pragma unroll
       for (int j = 0; j < R; ++j) {
         S[i][j] = P[i][j] + Q[i][j];
         PAt[i][j] = P[i][j];
+      }
+  } else if constexpr (AI == kADiag) {
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+#pragma unroll
+      for (int j = 0; j < R; ++j) {
+        PAt[i][j] = P[i][j] * A[j][j];
+        S[i][j] = A[i][i] * PAt[i][j] + (i == j ? Q[i][i] : 0.0);
       }
   } else {
     matmul_nt<R, R, R>(P, A, PAt);
@@ -319,9 +448,12 @@ EKS_DEV bool rts_gain(const double (&m)[R], const double (&P)[R][R], const doubl
   const bool ok = small_inverse<R>(S, Si);
   matmul<R, R, R>(PAt, Si, J);
   double Am[R];
-  if constexpr (AI) {
+  if constexpr (AI == kAId) {
 #pragma unroll
     for (int i = 0; i < R; ++i) Am[i] = m[i];
+  } else if constexpr (AI == kADiag) {
+#pragma unroll
+    for (int i = 0; i < R; ++i) Am[i] = A[i][i] * m[i];
   } else {
     matvec<R, R>(A, m, Am);
   }
@@ -335,13 +467,23 @@ EKS_DEV bool rts_gain(const double (&m)[R], const double (&P)[R][R], const doubl
   return ok;
 }
 
-template <int R, int N, bool CI>
+template <int R, int N, int CI>
 EKS_DEV void project_store(double *out, long long oj, const double (&C)[N][R],
                            const double (&ms)[R], const double (&off)[N]) {
+  if constexpr (CI == kCPupil) {
+    static_assert(R == 3 && N == 8, "the pupil model is r = 3, n = 8");
+    const double o[8] = {cdot3<0, 2, 0>(ms[0], ms[1], ms[2]), cdot3<-1, 0, 2>(ms[0], ms[1], ms[2]),
+                         cdot3<0, 2, 0>(ms[0], ms[1], ms[2]), cdot3<1, 0, 2>(ms[0], ms[1], ms[2]),
+                         cdot3<1, 2, 0>(ms[0], ms[1], ms[2]), cdot3<0, 0, 2>(ms[0], ms[1], ms[2]),
+                         cdot3<-1, 2, 0>(ms[0], ms[1], ms[2]), cdot3<0, 0, 2>(ms[0], ms[1], ms[2])};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) out[j * oj] = o[j] + off[j];
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < N; ++j) {
     double cm;
-    if constexpr (CI) {
+    if constexpr (CI == kCId) {
       cm = ms[j];
     } else {
       cm = 0.0;
@@ -425,6 +567,54 @@ struct Elem {
   }
 };
 
+// One scalar observation y ~ N(c x_t, r) absorbed into the element, given
+// v = Cb c, g = Ab^T c, s = c Cb c + r, hb = c bb.
+template <int R>
+EKS_DEV void absorb_scalar(Elem<R> &E, const double (&v)[R], const double (&g)[R], double s,
+                           double hb, double y, bool &ok, NllAcc *acc) {
+  ok = ok && !(s <= 0.0);
+  const double inv = rcp_nr(s);
+  const double e0 = y - hb;
+  const double ei = e0 * inv;
+  if (acc) acc->add(e0, s, inv);
+#pragma unroll
+  for (int a = 0; a < R; ++a) {
+    const double ga = g[a] * inv;
+    E.eta[a] = fma(g[a], ei, E.eta[a]);
+#pragma unroll
+    for (int c = a; c < R; ++c) {
+      E.Jb[a][c] = fma(ga, g[c], E.Jb[a][c]);
+      if (c != a) E.Jb[c][a] = E.Jb[a][c];
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < R; ++a) {
+    const double ka = v[a] * inv;
+    E.bb[a] = fma(ka, e0, E.bb[a]);
+#pragma unroll
+    for (int c = 0; c < R; ++c) E.Ab[a][c] = fma(-ka, g[c], E.Ab[a][c]);
+#pragma unroll
+    for (int c = a; c < R; ++c) {
+      E.Cb[a][c] = fma(-ka, v[c], E.Cb[a][c]);
+      if (c != a) E.Cb[c][a] = E.Cb[a][c];
+    }
+  }
+}
+
+// the same for pupil row H (sparse c)
+template <int H0, int H1, int H2>
+EKS_DEV void absorb_row(Elem<3> &E, double y, double r, bool &ok, NllAcc *acc) {
+  double v[3], g[3];
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    v[a] = cdot3<H0, H1, H2>(E.Cb[a][0], E.Cb[a][1], E.Cb[a][2]);
+    g[a] = cdot3<H0, H1, H2>(E.Ab[0][a], E.Ab[1][a], E.Ab[2][a]);
+  }
+  const double s = r + cdot3<H0, H1, H2>(v[0], v[1], v[2]);
+  const double hb = cdot3<H0, H1, H2>(E.bb[0], E.bb[1], E.bb[2]);
+  absorb_scalar<3>(E, v, g, s, hb, y, ok, acc);
+}
+
 // Absorb one time step (predict with A, Q; update with the N scalar
 // observations of y, rv) into the running element.
 // With `acc`, the step's terms of the element's likelihood constant are
@@ -433,11 +623,11 @@ struct Elem {
 //   -log p(y_{s..e-1} | x) = K + 1/2 x^T Jb x - eta^T x,
 //   K = 1/2 sum_i (log 2 pi + log s_i + e0_i^2 / s_i)   (acc.value)
 // which elem_nll_share turns into the chunk's NLL share.
-template <int R, int N, bool AI, bool CI>
+template <int R, int N, int AI, int CI>
 EKS_DEV void elem_absorb(Elem<R> &E, const double (&A)[R][R], const double (&Q)[R][R],
                          const double (&C)[N][R], const double (&y)[N], const double (&rv)[N],
                          bool &ok, NllAcc *acc = nullptr) {
-  if constexpr (AI) {
+  if constexpr (AI == kAId) {
 #pragma unroll
     for (int i = 0; i < R; ++i)
 #pragma unroll
@@ -445,6 +635,19 @@ EKS_DEV void elem_absorb(Elem<R> &E, const double (&A)[R][R], const double (&Q)[
         E.Cb[i][j] += Q[i][j];
         if (j != i) E.Cb[j][i] = E.Cb[i][j];
       }
+  } else if constexpr (AI == kADiag) {  // A, Q diagonal
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+#pragma unroll
+      for (int j = 0; j < R; ++j) E.Ab[i][j] *= A[i][i];
+      E.bb[i] *= A[i][i];
+#pragma unroll
+      for (int j = i; j < R; ++j) {
+        const double t = (A[i][i] * E.Cb[i][j]) * A[j][j];
+        E.Cb[i][j] = (i == j) ? t + Q[i][i] : t;
+        if (j != i) E.Cb[j][i] = E.Cb[i][j];
+      }
+    }
   } else {
     double T1[R][R], T2[R][R], b2[R];
     matmul<R, R, R>(A, E.Ab, T1);
@@ -470,10 +673,24 @@ EKS_DEV void elem_absorb(Elem<R> &E, const double (&A)[R][R], const double (&Q)[
 #pragma unroll
       for (int j = 0; j < i; ++j) E.Cb[i][j] = E.Cb[j][i];
   }
+  if constexpr (CI == kCPupil) {
+    static_assert(R == 3 && N == 8, "the pupil model is r = 3, n = 8");
+    double ya, ra, yb, rb;
+    merge_obs(y[0], rv[0], y[2], rv[2], ya, ra, acc, ok);
+    merge_obs(y[5], rv[5], y[7], rv[7], yb, rb, acc, ok);
+    absorb_row<0, 2, 0>(E, ya, ra, ok, acc);
+    absorb_row<-1, 0, 2>(E, y[1], rv[1], ok, acc);
+    absorb_row<1, 0, 2>(E, y[3], rv[3], ok, acc);
+    absorb_row<1, 2, 0>(E, y[4], rv[4], ok, acc);
+    absorb_row<0, 0, 2>(E, yb, rb, ok, acc);
+    absorb_row<-1, 2, 0>(E, y[6], rv[6], ok, acc);
+    if (acc) acc->renorm();
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < N; ++i) {
     double v[R], g[R], s, hb;
-    if constexpr (CI) {
+    if constexpr (CI == kCId) {
 #pragma unroll
       for (int a = 0; a < R; ++a) {
         v[a] = E.Cb[a][i];
@@ -501,33 +718,7 @@ EKS_DEV void elem_absorb(Elem<R> &E, const double (&A)[R][R], const double (&Q)[
         hb = fma(C[i][k], E.bb[k], hb);
       }
     }
-    ok = ok && !(s <= 0.0);
-    const double inv = rcp_nr(s);
-    const double e0 = y[i] - hb;
-    const double ei = e0 * inv;
-    if (acc) acc->add(e0, s, inv);
-#pragma unroll
-    for (int a = 0; a < R; ++a) {
-      const double ga = g[a] * inv;
-      E.eta[a] = fma(g[a], ei, E.eta[a]);
-#pragma unroll
-      for (int c = a; c < R; ++c) {
-        E.Jb[a][c] = fma(ga, g[c], E.Jb[a][c]);
-        if (c != a) E.Jb[c][a] = E.Jb[a][c];
-      }
-    }
-#pragma unroll
-    for (int a = 0; a < R; ++a) {
-      const double ka = v[a] * inv;
-      E.bb[a] = fma(ka, e0, E.bb[a]);
-#pragma unroll
-      for (int c = 0; c < R; ++c) E.Ab[a][c] = fma(-ka, g[c], E.Ab[a][c]);
-#pragma unroll
-      for (int c = a; c < R; ++c) {
-        E.Cb[a][c] = fma(-ka, v[c], E.Cb[a][c]);
-        if (c != a) E.Cb[c][a] = E.Cb[a][c];
-      }
-    }
+    absorb_scalar<R>(E, v, g, s, hb, y[i], ok, acc);
   }
   if (acc) acc->renorm();
 }

@@ -128,7 +128,9 @@ inline bool uniform_lanes(long long B);
 // L balances the per-lane serial chunk work (~ L steps) against the serial
 // part of the block-parallel chunk scans (~ 2 NC / 512 element compositions):
 // L = sqrt(2 T rho / 512), rho = composition / step cost ratio, measured 2.6
-// for r <= 2 and 1.3 for r = 3 (configs 2, 3, 5: EKS_CHUNK_LEN sweeps).
+// for r <= 2 and 0.8 for r = 3 (configs 2, 3, 5: EKS_CHUNK_LEN sweeps; config
+// 5 with the pupil kernels and the prefetched K2: L = 40 / 56 / 72 / 96 ->
+// 3.41 / 3.20 / 3.33 / ~3.5 ms per step, tools/c5_sweep.sh).
 inline long long chunk_len(long long B, long long T, int r) {
   const long long ls = 8;  // a multiple of every checkpoint interval
   static const long long forced = [] {  // EKS_CHUNK_LEN: tuning experiments only
@@ -143,7 +145,7 @@ inline long long chunk_len(long long B, long long T, int r) {
     const long long l_scan = (long long)std::ceil(std::sqrt(2.0 * (double)T / 64.0));
     L = std::max(kMinChunk, std::max(l_fill, l_scan));
   } else {
-    const double rho = r <= 2 ? 2.6 : 1.3;
+    const double rho = r <= 2 ? 2.6 : 0.8;
     L = std::max(kMinChunk, (long long)std::llround(std::sqrt(2.0 * (double)T * rho / 512.0)));
   }
   L = round_up(L, ls);
@@ -160,6 +162,8 @@ struct ChunkPlan {
   // constant, K2 adds the start-state terms: elem_nll_share), so K3 does not
   // re-run the filter
   int nll_closed = 0;
+  // ... and the wave-parallel K2 sums the shares itself (no K4 NLL launch)
+  int nll_fused = 0;
   // members shared by all trajectories (batch stride 0, e.g. candidate models
   // of one trajectory): y / ev are stored once, as a single plane column
   long long yB = 0;
@@ -217,11 +221,13 @@ struct Model {
     load_mat<N, R>(pp + L::C, C);
     load_vec<N>(pp + L::off, off);
   }
-  template <bool AI, bool CI>
+  template <int AI, int CI>
   EKS_DEV bool valid() const {
     bool ok = true;
-    if constexpr (AI) ok = ok && is_identity<R>(A);
-    if constexpr (CI) ok = ok && is_identity_rect<N, R>(C);
+    if constexpr (AI == kAId) ok = ok && is_identity<R>(A);
+    if constexpr (AI == kADiag) ok = ok && is_diagonal<R>(A) && is_diagonal<R>(Q);
+    if constexpr (CI == kCId) ok = ok && is_identity_rect<N, R>(C);
+    if constexpr (CI == kCPupil) ok = ok && is_pupil_c<N, R>(C);
     return ok;
   }
 };
@@ -303,7 +309,7 @@ struct yev_y<YevIn<YT>> {
 // ===========================================================================
 // algo 1: one lane per trajectory, sequential in time
 // ===========================================================================
-template <int R, int N, int E, typename T, bool AI, bool CI>
+template <int R, int N, int E, typename T, int AI, int CI>
 __global__ __launch_bounds__(64) void k_smooth_seq(SmoothArgs a) {
   constexpr int K = R + Sym<R>::len;
   constexpr int EE = E > 0 ? E : 1;
@@ -587,8 +593,8 @@ __global__ __launch_bounds__(kBlock) void k_c0_shared(SmoothArgs a, ChunkPlan p)
   }
 }
 
-template <int R, int N, int E, typename T, typename YT, bool AI, bool CI, bool UNI>
-__global__ __launch_bounds__(kBlock) void k_c1_elem(SmoothArgs a, ChunkPlan p) {
+template <int R, int N, int E, typename T, typename YT, int AI, int CI, bool UNI>
+EKS_DEV __forceinline__ void c1_elem_body(const SmoothArgs &a, const ChunkPlan &p) {
   constexpr int D = (E > 0 && E * N <= 16) ? 2 : 1;  // member prefetch distance (steps)
   Lane<UNI> ln;
   const long long B = a.B, TT = a.T;
@@ -640,6 +646,30 @@ __global__ __launch_bounds__(kBlock) void k_c1_elem(SmoothArgs a, ChunkPlan p) {
   }
   El.store((double *)(a.ws + p.elem_off) + ((long long)b * p.NC + c) * Elem<R>::len, 1);
   if (!ok) flag(a.status, b, first ? EKS_STATUS_SINGULAR : EKS_STATUS_SCAN);
+}
+
+template <int R, int N, int E, typename T, typename YT, int AI, int CI, bool UNI>
+__global__ __launch_bounds__(kBlock) void k_c1_elem(SmoothArgs a, ChunkPlan p) {
+  c1_elem_body<R, N, E, T, YT, AI, CI, UNI>(a, p);
+}
+
+// The same with at least W waves per SIMD (VGPRs <= 512 / W).  The r = 3
+// element build from y / ev planes (the shared-member sweep of config 5)
+// needs ~230-280 VGPRs unconstrained, i.e. ONE wave per SIMD, and its
+// per-step chain of dependent scalar updates is then latency bound.
+template <int R, int N, int E, typename T, typename YT, int AI, int CI, bool UNI, int W>
+__global__ __launch_bounds__(kBlock, W) void k_c1_elem_occ(SmoothArgs a, ChunkPlan p) {
+  c1_elem_body<R, N, E, T, YT, AI, CI, UNI>(a, p);
+}
+
+// waves per SIMD of k_c1_elem_occ (EKS_C1_WPE: tuning experiments; 0 = the
+// unconstrained kernel)
+inline int c1_waves_per_simd() {
+  static const int v = [] {
+    const char *e = getenv("EKS_C1_WPE");
+    return e ? atoi(e) : 2;
+  }();
+  return v;
 }
 
 template <int R, int N>
@@ -714,12 +744,16 @@ __global__ __launch_bounds__(64 * W) void k_c2_fscan_w(SmoothArgs a, ChunkPlan p
   bool ok = true;
   Elem<R> agg;
   agg.set_identity();
-  for (long long c = c0; c < c1; ++c) {
-    Elem<R> e;
-    e.load(elem + (b * NC + c) * Elem<R>::len, 1);
-    Elem<R> t;
-    ok = compose_elem<R>(agg, e, t) && ok;
-    agg = t;
+  {  // the chain is latency bound: the next element is in flight while one is composed
+    Elem<R> nx;
+    if (c0 < c1) nx.load(elem + (b * NC + c0) * Elem<R>::len, 1);
+    for (long long c = c0; c < c1; ++c) {
+      const Elem<R> e = nx;
+      if (c + 1 < c1) nx.load(elem + (b * NC + c + 1) * Elem<R>::len, 1);
+      Elem<R> t;
+      ok = compose_elem<R>(agg, e, t) && ok;
+      agg = t;
+    }
   }
 #pragma unroll
   for (int k = 1; k < 64; k <<= 1) {
@@ -753,6 +787,7 @@ __global__ __launch_bounds__(64 * W) void k_c2_fscan_w(SmoothArgs a, ChunkPlan p
       }
     }
   }
+  double nsum = 0.0;  // this thread's NLL shares (nll_fused)
   if (c0 < c1 && a.t_base > 0) {
     // a later time segment: every thread starts from the handed-over state
     // composed with the elements before its first chunk
@@ -794,14 +829,34 @@ __global__ __launch_bounds__(64 * W) void k_c2_fscan_w(SmoothArgs a, ChunkPlan p
       }
     }
     double *np_ = (double *)(a.ws + p.nllp_off);
+    const bool need = !p.nll_closed;  // the start states feed K3 / K5 (not a closed-form NLL call)
+    Elem<R> nx;
+    if (c < c1) nx.load(elem + (b * NC + c) * Elem<R>::len, 1);
     for (; c < c1; ++c) {
-      store_state<R>(cst + (c * KS) * B + b, B, m, P);
+      if (need) store_state<R>(cst + (c * KS) * B + b, B, m, P);
       if (c + 1 < c1 || p.nll_closed) {
-        Elem<R> e;
-        e.load(elem + (b * NC + c) * Elem<R>::len, 1);
-        if (p.nll_closed) np_[c * B + b] = elem_nll_share<R>(m, P, e, np_[c * B + b], ok);
+        const Elem<R> e = nx;
+        if (c + 1 < c1) nx.load(elem + (b * NC + c + 1) * Elem<R>::len, 1);
+        if (p.nll_closed) {
+          const double sh = elem_nll_share<R>(m, P, e, np_[c * B + b], ok);
+          if (p.nll_fused) nsum += sh;
+          else np_[c * B + b] = sh;
+        }
         if (c + 1 < c1) ok = compose_state<R>(m, P, e) && ok;
       }
+    }
+    if (tid == 0 && p.nll_fused) nsum += np_[b];  // chunk 0's share: the plain filter's (K1)
+  }
+  if (p.nll_fused) {  // the NLL sum: per thread in chunk order, then the block (fixed order)
+#pragma unroll
+    for (int k = 32; k >= 1; k >>= 1) nsum += __shfl_xor(nsum, k, 64);
+    __shared__ double ns[W];
+    if (l == 0) ns[w] = nsum;
+    __syncthreads();
+    if (tid == 0) {
+      double t = ns[0];
+      for (int v = 1; v < W; ++v) t += ns[v];
+      a.nll[b] = t;
     }
   }
   if (!ok) flag(a.status, b, EKS_STATUS_SCAN);
@@ -872,7 +927,15 @@ __global__ __launch_bounds__(64 * W) void k_c4_bscan_w(SmoothArgs a, ChunkPlan p
   auto map_of = [&](long long c) { return load_map(bw + (b * NC + c) * (R * R + R)); };
   Affine<R> F;
   F.set_identity();
-  for (long long c = c1 - 1; c >= c0; --c) F = map_of(c).after(F);
+  {  // latency bound: the next map is in flight while one is composed
+    Affine<R> nx;
+    if (c1 > c0) nx = map_of(c1 - 1);
+    for (long long c = c1 - 1; c >= c0; --c) {
+      const Affine<R> f = nx;
+      if (c - 1 >= c0) nx = map_of(c - 1);
+      F = f.after(F);
+    }
+  }
 #pragma unroll
   for (int k = 1; k < 64; k <<= 1) {
     const Affine<R> o = F.shfl_down(k);
@@ -907,12 +970,15 @@ __global__ __launch_bounds__(64 * W) void k_c4_bscan_w(SmoothArgs a, ChunkPlan p
       for (int k = 0; k < R; ++k) t = fma(X.G[i][k], a.seg_in[b * R + k], t);
     ms[i] = t;
   }
+  Affine<R> nxm;
+  if (c1 > c0) nxm = map_of(c1 - 1);
   for (long long c = c1 - 1; c >= c0; --c) {
     if (c + 1 < NC || a.seg_in) {
 #pragma unroll
       for (int i = 0; i < R; ++i) msend[(c * R + i) * B + b] = ms[i];
     }
-    const Affine<R> f = map_of(c);
+    const Affine<R> f = nxm;
+    if (c - 1 >= c0) nxm = map_of(c - 1);
     double nx[R];
 #pragma unroll
     for (int i = 0; i < R; ++i) {
@@ -1111,7 +1177,7 @@ EKS_DEV void load_yev(const YT *ybuf, const double *evbuf, long long t, long lon
   }
 }
 
-template <int R, int N, typename YT, bool AI, bool CI, int LS, bool UNI>
+template <int R, int N, typename YT, int AI, int CI, int LS, bool UNI>
 __global__ __launch_bounds__(kBlock) void k_c3_rerun(SmoothArgs a, ChunkPlan p) {
   // y / ev prefetch distance (steps; divides LS): 2 keeps the (2, 2) kernel at
   // 3 waves/SIMD (160 VGPRs), measured 3 % faster than 4 (174 VGPRs, 2 waves)
@@ -1278,7 +1344,7 @@ __global__ __launch_bounds__(64) void k_c4_nll(SmoothArgs a, ChunkPlan p) {
   if (l == 0) a.nll[b] = s;
 }
 
-template <int R, int N, typename YT, bool AI, bool CI, int LS, bool UNI>
+template <int R, int N, typename YT, int AI, int CI, int LS, bool UNI>
 __global__ __launch_bounds__(kBlock) void k_c5_final(SmoothArgs a, ChunkPlan p) {
   Lane<UNI> ln;
   const long long B = a.B, TT = a.T;
@@ -1379,7 +1445,7 @@ int dispatch_members_c(int E, F &&f) {
 
 #include "two_pass.hpp"
 
-template <int R, int N, bool AI, bool CI>
+template <int R, int N, int AI, int CI>
 int launch_shape(const SmoothArgs &a, int algo, long long L) {
   if (algo == 3) return launch_algo3<R, N, AI, CI>(a);
   const bool f32 = a.dtype == EKS_F32;
@@ -1414,6 +1480,7 @@ int launch_shape(const SmoothArgs &a, int algo, long long L) {
   ChunkPlan p = make_plan(a.B, a.T, R, N, L);
   p.smooth = a.out != nullptr;
   p.nll_closed = (!p.smooth && a.phase == 0 && a.nll) ? 1 : 0;
+  p.nll_fused = (p.nll_closed && p.NC > wave_scan_chunks()) ? 1 : 0;
   const bool shared = !yev && a.sb == 0 && a.B > 1;
   p.yB = shared ? 1 : a.B;
   const bool uni = uniform_lanes(a.B);
@@ -1442,8 +1509,21 @@ int launch_shape(const SmoothArgs &a, int algo, long long L) {
       auto k1 = [&](auto Ec) {
         constexpr int EE = decltype(Ec)::value;
         prof_mark(a.stream, "k_c1_elem");
-        hipLaunchKernelGGL((k_c1_elem<R, N, EE, Tp, YT, AI, CI, U>), dim3(gch), dim3(kBlock), 0,
-                           a.stream, a, p);
+        if constexpr (R == 3 && is_yev<Tp>::value) {
+          const int w = c1_waves_per_simd();
+          if (w == 2)
+            hipLaunchKernelGGL((k_c1_elem_occ<R, N, EE, Tp, YT, AI, CI, U, 2>), dim3(gch),
+                               dim3(kBlock), 0, a.stream, a, p);
+          else if (w == 3)
+            hipLaunchKernelGGL((k_c1_elem_occ<R, N, EE, Tp, YT, AI, CI, U, 3>), dim3(gch),
+                               dim3(kBlock), 0, a.stream, a, p);
+          else
+            hipLaunchKernelGGL((k_c1_elem<R, N, EE, Tp, YT, AI, CI, U>), dim3(gch), dim3(kBlock),
+                               0, a.stream, a, p);
+        } else {
+          hipLaunchKernelGGL((k_c1_elem<R, N, EE, Tp, YT, AI, CI, U>), dim3(gch), dim3(kBlock), 0,
+                             a.stream, a, p);
+        }
         return check_launch("k_c1_elem");
       };
       if constexpr (is_yev<Tp>::value)
@@ -1485,6 +1565,10 @@ int launch_shape(const SmoothArgs &a, int algo, long long L) {
         hipLaunchKernelGGL((k_c2_fscan_w<R, N, 1>), dim3((unsigned)a.B), dim3(64), 0, a.stream,
                            a, p);
       if ((rc = check_launch("k_c2_fscan"))) return rc;
+      if (p.nll_fused) {  // K2 summed the closed-form NLL shares: done
+        prof_call_end(a.stream);
+        return 0;
+      }
       if (!p.nll_closed) {
         prof_mark(a.stream, "k_c3_rerun");
         hipLaunchKernelGGL((k_c3_rerun<R, N, YT, AI, CI, LS, U>), dim3(gch), dim3(kBlock), 0,

@@ -196,7 +196,7 @@ EKS_DEV void load_elem_pl(const double *base, long long c, long long B, unsigned
 // ---------------------------------------------------------------------------
 // P1: fine elements + coarse aggregates
 // ---------------------------------------------------------------------------
-template <int R, int N, int E, typename T, bool AI, bool CI>
+template <int R, int N, int E, typename T, int AI, int CI>
 __global__ __launch_bounds__(64 * kWV) EKS_K3E_WPE void k3_elem(SmoothArgs a, Plan3 p) {
   constexpr int EL = Elem<R>::len;
   constexpr int D = EKS_K3_D;
@@ -643,7 +643,7 @@ __global__ __launch_bounds__(kBlock) void k3_fine(SmoothArgs a, Plan3 p) {
 // ---------------------------------------------------------------------------
 // P4: final smoothing pass
 // ---------------------------------------------------------------------------
-template <int R, int N, int E, typename T, typename YT, bool AI, bool CI, int LS>
+template <int R, int N, int E, typename T, typename YT, int AI, int CI, int LS>
 __global__ __launch_bounds__(kBlock) void k3_final(SmoothArgs a, Plan3 p) {
   constexpr int KS = R + Sym<R>::len;
   constexpr int D = EKS_K3_DF;
@@ -751,7 +751,7 @@ __global__ __launch_bounds__(kBlock) void k3_final(SmoothArgs a, Plan3 p) {
             double cm[2];
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
-              if constexpr (CI) {
+              if constexpr (CI == kCId) {
                 cm[j] = ms[j] + md.off[j];
               } else {
                 double u = 0.0;
@@ -805,7 +805,7 @@ __global__ __launch_bounds__(kBlock) void k3_final(SmoothArgs a, Plan3 p) {
 // step (LDS for the early sub-chunks, registers for the last one) instead of
 // (y, ev), so the backward sweep computes the RTS gains without re-running
 // the filter (one filter pass per step instead of 1.5).
-template <int R, int N, int E, typename T, typename YT, bool AI, bool CI, int LS, bool WALK>
+template <int R, int N, int E, typename T, typename YT, int AI, int CI, int LS, bool WALK>
 __global__ __launch_bounds__(kBlock) EKS_K3_WPE void k3_final_s(SmoothArgs a, Plan3 p) {
   constexpr int KS = R + Sym<R>::len;
   constexpr int D = EKS_K3_DF;
@@ -984,7 +984,7 @@ __global__ __launch_bounds__(kBlock) EKS_K3_WPE void k3_final_s(SmoothArgs a, Pl
         double cm[2];
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-          if constexpr (CI) {
+          if constexpr (CI == kCId) {
             cm[j] = ms[j] + md.off[j];
           } else {
             double u = 0.0;
@@ -1067,7 +1067,7 @@ __global__ __launch_bounds__(64) void k3_nll(SmoothArgs a, Plan3 p) {
 }
 
 // host: the four (five with NLL) launches of one algo-3 call
-template <int R, int N, bool AI, bool CI>
+template <int R, int N, int AI, int CI>
 int launch_algo3(const SmoothArgs &a) {
   constexpr int LS = sub_len_c(R, N);
   const Plan3 p = make_plan3(a.B, a.T, R, N);

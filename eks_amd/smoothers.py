@@ -32,7 +32,7 @@ def _run_fused(stack: np.ndarray, model: dict, mode: str = "median", want_ms=Fal
     params = batch.pack_params(model["m0"], model["S0"], model["A"], model["Q"], model["C"],
                                model["offset"])
     res = batch.smooth(obs, params, n=n, r=r, mode=mode, want_ms=want_ms, want_nll=want_nll,
-                       flags=batch.model_flags(model["A"], model["C"]), check=True)
+                       flags=batch.model_flags(model["A"], model["C"], model["Q"]), check=True)
     out = res["out"][0].cpu().numpy()
     ms = res["ms"][0].cpu().numpy() if want_ms else None
     nll = float(res["nll"][0].item()) if want_nll else None
@@ -113,7 +113,9 @@ def pupil_smoothing_sweep(markers_list, keypoint_names, tracker_name, diameter_s
     params = batch.pack_params(stackp("m0"), stackp("S0"), stackp("A"), stackp("Q"),
                                stackp("C"), stackp("offset"))
     obs = torch.from_numpy(np.ascontiguousarray(stack)).to("cuda").permute(1, 0, 2).unsqueeze(0)
-    scores = batch.nll(obs.expand(len(grid), -1, -1, -1), params, n=n, r=3).cpu().numpy()
+    flags = batch.model_flags(stackp("A"), stackp("C"), stackp("Q"))
+    scores = batch.nll(obs.expand(len(grid), -1, -1, -1), params, n=n, r=3,
+                       flags=flags).cpu().numpy()
     best = grid[int(np.argmin(scores))]
     res = ensemble_kalman_smoother_pupil(markers_list, keypoint_names, tracker_name,
                                          np.diag([best[0], best[1], best[1]]))

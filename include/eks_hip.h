@@ -25,8 +25,9 @@
  *       EKS_STATUS_SINGULAR   a matrix the reference would hand to
  *                             np.linalg.solve was singular (the reference
  *                             raises LinAlgError there)
- *       EKS_STATUS_BAD_MODEL  a model_flags promise (A or C = identity) does
- *                             not hold for this trajectory's parameters
+ *       EKS_STATUS_BAD_MODEL  a model_flags promise (A or C = identity, the
+ *                             pupil structure) does not hold for this
+ *                             trajectory's parameters
  *       EKS_STATUS_SCAN       the time-parallel scan could not form a chunk
  *                             summary (singular Q with exact observations);
  *                             rerun that batch with algo = 1
@@ -53,7 +54,7 @@ enum {
 enum { EKS_STATUS_SINGULAR = 1, EKS_STATUS_BAD_MODEL = 2, EKS_STATUS_SCAN = 4 };
 
 /* model structure promises for eks_smooth (verified per trajectory) */
-enum { EKS_MODEL_A_IDENTITY = 1, EKS_MODEL_C_IDENTITY = 2 };
+enum { EKS_MODEL_A_IDENTITY = 1, EKS_MODEL_C_IDENTITY = 2, EKS_MODEL_PUPIL = 4 };
 
 enum { EKS_F32 = 0, EKS_F64 = 1 };
 /* eks_smooth input that is not member predictions but the ensemble output
@@ -160,7 +161,12 @@ int64_t eks_param_len(int n, int r);
  *   model_flags  EKS_MODEL_A_IDENTITY / EKS_MODEL_C_IDENTITY: the caller
  *            promises A = I (and C = I, r = n) for every trajectory, which
  *            selects kernels that skip those products (single-view: both;
- *            multi-camera: A).  Violations are flagged in `status`.
+ *            multi-camera: A).  EKS_MODEL_PUPIL (r = 3, n = 8): C is the
+ *            pupil measurement matrix of eks/pupil_smoother.py:150-153 (rows
+ *            in the order top x, y, bottom x, y, right x, y, left x, y) and A,
+ *            Q are diagonal (:140-147): sparse updates, the two pairs of
+ *            equal rows folded into one observation each.  Violations are
+ *            flagged in `status`.
  *   workspace / workspace_bytes: device scratch of at least
  *            eks_smooth_workspace_bytes(...) bytes (not zeroed by caller).
  *   algo     0 = automatic, 1 = sequential (one lane per trajectory),

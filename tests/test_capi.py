@@ -93,3 +93,40 @@ def test_torch_ops_registered_with_fake_shapes():
         assert torch.ops.eks.nll(obs, params, 2, 2, "median", 0).shape == (3,)
     with pytest.raises(RuntimeError, match="GPU only"):
         torch.ops.eks.ensemble(torch.zeros((1, 4, 3, 2)), "median")
+
+
+def test_header_enums_match_bindings():
+    """Every enum constant the header defines has the same value in _lib."""
+    import os
+    import re
+    hdr = open(os.path.join(os.path.dirname(_lib.__file__), "..", "include", "eks_hip.h")).read()
+    consts = dict(re.findall(r"\b(EKS_[A-Z0-9_]+)\s*=\s*(-?\d+)", hdr))
+    assert "EKS_MODEL_PUPIL" in consts
+    for name, val in consts.items():
+        if hasattr(_lib, name):
+            assert getattr(_lib, name) == int(val), name
+
+
+def test_model_flags_pupil_structure():
+    """batch.model_flags: the pupil promise needs C = the pupil matrix
+    (eks/pupil_smoother.py:150-153) and diagonal A and Q."""
+    import numpy as np
+    from eks_amd import batch, fit
+    A = np.diag([0.99, 0.999, 0.999])
+    Q = np.diag([1.0, 2.0, 3.0])
+    assert batch.model_flags(A, fit.PUPIL_C, Q) == _lib.EKS_MODEL_PUPIL
+    assert batch.model_flags(np.stack([A, A]), np.stack([fit.PUPIL_C] * 2),
+                             np.stack([Q, Q])) == _lib.EKS_MODEL_PUPIL
+    assert batch.model_flags(A, fit.PUPIL_C) == 0           # Q unknown: no promise
+    Qb = Q.copy()
+    Qb[0, 1] = 1e-3
+    assert batch.model_flags(A, fit.PUPIL_C, Qb) == 0
+    Cb = fit.PUPIL_C.copy()
+    Cb[1, 0] = -0.49
+    assert batch.model_flags(A, Cb, Q) == 0
+    assert batch.model_flags(np.eye(3), fit.PUPIL_C, Q) == (_lib.EKS_MODEL_A_IDENTITY
+                                                           | _lib.EKS_MODEL_PUPIL)
+    # the pupil model the wrappers fit
+    preds = np.random.default_rng(0).normal(50, 2, size=(400, 8))
+    m = fit.pupil_model(preds, np.diag([0.9, 0.99, 0.99]))
+    assert batch.model_flags(m["A"], m["C"], m["Q"]) == _lib.EKS_MODEL_PUPIL
