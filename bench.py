@@ -45,6 +45,7 @@ sys.path.insert(0, HERE)
 
 METRIC = "keypoint-timesteps smoothed/sec at 1/2/4/8 MI355X; max|Δ| vs CPU"
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+PEAK_FP64_TFS = 78.6   # MI355X FP64 vector peak (AMD spec: half the 157.3 TF/s FP32 vector rate)
 
 
 def parse():
@@ -435,6 +436,13 @@ def workload_pupil(torch, a, dev, rank, world):
     return dict(step=step_timeshard if a.timeshard else step, status=status, units=4 * Tk,
                 bytes_per_unit=(32 * E + 88) / 4, cpu_plan=cpu_plan, desc=desc,
                 timeshard=a.timeshard,
+                # k_c1_elem: one element-absorb step per (candidate, frame); flops counted
+                # from kf_steps.hpp elem_absorb (FMA = 2): pupil kernels 27 (diagonal
+                # predict) + 42 (two folded pairs) + 2 x 76 + 4 x 92 (sparse rows) = 589;
+                # dense r = 3, n = 8: 162 + 8 x 123 = 1146
+                flops=dict(kernel="k_c1_elem", per_unit=1146 if a.dense_pupil else 589,
+                           units=(len(cands) + 1) * Tk,  # the sweep + the chosen model's smooth
+                           unit_is="element-absorb step"),
                 cfg=dict(frames=T, keypoints=4, members=E, candidates=len(cands)),
                 shape=(1, T, 8, 3, E),
                 key=f"config5-pupil-t{T}-n{world}{'-ts' if a.timeshard else ''}",
@@ -668,6 +676,15 @@ def main():
             "setup_s": round(setup_s, 2),
             "hip_graph": graph is not None,
         }
+        if "flops" in w:  # an FP64-issue-bound kernel: its flop roofline beside the HBM one
+            f = w["flops"]
+            kms = dict(kernels).get(f["kernel"])
+            if kms:
+                tf = f["per_unit"] * f["units"] / (kms * 1e-3) / 1e12
+                line["flop_roofline"] = dict(kernel=f["kernel"], bound="fp64 valu", achieved=tf,
+                                             peak=PEAK_FP64_TFS, unit="TFLOP/s",
+                                             frac=tf / PEAK_FP64_TFS, flops_per_unit=f["per_unit"],
+                                             units_per_launch=f["units"], unit_is=f["unit_is"])
         if "extra" in w:
             line.update(w["extra"]())
         if world > 1:

@@ -115,7 +115,8 @@ def smooth(obs, params, *, n: int, r: int, mode: str = "median", out=None, want_
     that the kernel's stores are coalesced.  ``flags`` are EKS_MODEL_* promises
     (see ``model_flags``); ``algo`` 0 = automatic, 1 = sequential, 2 =
     time-parallel (three passes), 3 = time-parallel in two passes over the
-    members (include/eks_hip.h).  With ``check=True`` the call synchronises, raises on
+    members, 4 = the runtime-n sequential kernel that every (r, n) without
+    compiled kernels runs (include/eks_hip.h).  With ``check=True`` the call synchronises, raises on
     singular / mis-flagged trajectories and transparently re-runs with the
     sequential algorithm if the time-parallel scan reported a breakdown.
     """

@@ -12,7 +12,8 @@ constexpr double kLog2Pi = 1.8378770664093453;  // log(2 pi)
 constexpr double kLn2 = 0.6931471805599453;
 
 constexpr int kMaxLatent = 6;   // r
-constexpr int kMaxObs = 8;      // n
+constexpr int kMaxObs = 8;      // n (compiled kernels, eks_forward / eks_backward / eks_fit)
+constexpr int kMaxObsRt = 64;   // n of eks_smooth's runtime-n kernel (eks_shape_rt.hip)
 constexpr int kMaxMembers = 64; // E
 
 int set_err(int code, const char *fmt, ...);

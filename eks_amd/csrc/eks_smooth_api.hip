@@ -25,11 +25,21 @@ int pick_algo(long long B, long long T, int n, int r, int E, int algo) {
   return (a3_ok && many && r == 2 && n == 2) ? 3 : 2;
 }
 
-bool shape_supported(int r, int n) {
+bool shape_compiled(int r, int n) {
   return (r == 2 && n == 2) || (r == 3 && (n == 4 || n == 6 || n == 8));
 }
 
+// the runtime-n kernel (one lane per trajectory, any n <= kMaxObsRt): shapes
+// without compiled kernels, or any shape with algo = 4
+bool use_rt(int r, int n, int algo) {
+  return (r == 2 || r == 3) && n <= kMaxObsRt && (algo == 4 || !shape_compiled(r, n));
+}
+
 }  // namespace
+
+namespace eks {
+int launch_rt(const SmoothArgs &a);
+}
 
 extern "C" {
 
@@ -40,13 +50,15 @@ int64_t eks_smooth_chunk_len(int64_t B, int64_t T, int r) {
 }
 
 int eks_smooth_algo(int64_t B, int64_t T, int n, int r, int E, int algo) {
-  if (B <= 0 || T <= 0 || r < 1 || n < 1 || algo < 0 || algo > 3) return 0;
+  if (B <= 0 || T <= 0 || r < 1 || n < 1 || algo < 0 || algo > 4) return 0;
+  if (use_rt(r, n, algo)) return 4;
   return pick_algo(B, T, n, r, E, algo);
 }
 
 size_t eks_smooth_workspace_bytes(int64_t B, int64_t T, int n, int r, int E, int algo) {
   (void)E;
   if (B <= 0 || T <= 0 || r < 1 || n < 1) return 0;
+  if (use_rt(r, n, algo)) return seq_workspace_bytes(B, T, r);
   const int al = pick_algo(B, T, n, r, E, algo);
   if (al == 1) return seq_workspace_bytes(B, T, r);
   const size_t p2 = make_plan(B, T, r, n, chunk_len(B, T, r)).total;
@@ -71,16 +83,20 @@ static int smooth_call(const void *obs, int obs_dtype, int64_t B, int64_t T, int
   if (obs_dtype != EKS_F32 && obs_dtype != EKS_F64 && obs_dtype != EKS_YEV32 &&
       obs_dtype != EKS_YEV64)
     return set_err(EKS_ERR_ARG, "bad dtype");
-  if (algo < 0 || algo > 3) return set_err(EKS_ERR_ARG, "eks_smooth: algo %d unknown", algo);
-  if (!shape_supported(r, n))
+  if (algo < 0 || algo > 4) return set_err(EKS_ERR_ARG, "eks_smooth: algo %d unknown", algo);
+  const bool rt = use_rt(r, n, algo);
+  if (!rt && !shape_compiled(r, n))
     return set_err(EKS_ERR_UNSUPPORTED,
-                   "eks_smooth: (r=%d, n=%d) not compiled in (have (2,2) (3,4) (3,6) (3,8))", r, n);
+                   "eks_smooth: (r=%d, n=%d) not supported (compiled: (2,2) (3,4) (3,6) (3,8); "
+                   "any n <= %d for r = 2, 3)", r, n, kMaxObsRt);
+  if (rt && phase)
+    return set_err(EKS_ERR_UNSUPPORTED, "eks_smooth_seg: (r=%d, n=%d) has no time-parallel kernels", r, n);
   if ((model_flags & EKS_MODEL_C_IDENTITY) && r != n)
     return set_err(EKS_ERR_ARG, "eks_smooth: C = I needs r == n");
   if ((model_flags & EKS_MODEL_PUPIL) && (r != 3 || n != 8))
     return set_err(EKS_ERR_ARG, "eks_smooth: EKS_MODEL_PUPIL needs r = 3, n = 8");
   if (B == 0) return EKS_OK;
-  int al = phase ? 2 : pick_algo(B, T, n, r, E, algo);
+  int al = rt ? 4 : phase ? 2 : pick_algo(B, T, n, r, E, algo);
   const size_t need = phase ? make_plan(B, T, r, n, chunk_len(B, T, r)).total
                             : eks_smooth_workspace_bytes(B, T, n, r, E, al);
   if (!workspace || workspace_bytes < need)
@@ -97,6 +113,7 @@ static int smooth_call(const void *obs, int obs_dtype, int64_t B, int64_t T, int
   a.phase = phase;
   a.seg_in = seg_in;
   a.seg_out = seg_out;
+  if (rt) return launch_rt(a);  // model_flags are promises only: the general kernel serves all
   long long L = chunk_len(B, T, r);
   if (L >= T) L = (T + 7) / 8 * 8;
   if (r == 2 && n == 2) return launch_22(a, al, L);

@@ -37,6 +37,10 @@ def test_limits_and_sizes():
     assert lib.eks_smooth_algo(1 << 20, 1000, 2, 2, 5, 0) == 1
     assert lib.eks_smooth_algo(17408, 10000, 2, 2, 11, 3) == 2  # E = 11: no algo-3 kernels
     assert lib.eks_smooth_algo(4, 100, 2, 2, 5, 9) == 0
+    # shapes without compiled kernels (five cameras: n = 10) run the runtime-n kernel
+    assert lib.eks_smooth_algo(17, 50000, 10, 3, 5, 0) == 4
+    assert lib.eks_smooth_algo(17, 50000, 8, 3, 5, 4) == 4
+    assert lib.eks_smooth_workspace_bytes(17, 1000, 10, 3, 5, 0) == 17 * 1000 * 9 * 8
     assert lib.eks_smooth_workspace_bytes(17, 100000, 2, 2, 5, 2) >= 17 * 100000 * 2 * 16
 
 

@@ -1,0 +1,93 @@
+"""eks_smooth's runtime-n kernel (algo 4, eks_shape_rt.hip): any number of
+observed coordinates -- the multi-camera model with V > 4 cameras, which the
+reference accepts (eks/multiview_pca_smoother.py:641-666) -- against the
+oracle, and equal to the compiled general-C kernels (to ~1 ulp) where both exist.
+"""
+import numpy as np
+import pandas as pd
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+@pytest.mark.parametrize("V,T", [(5, 600), (8, 300)])
+def test_multicam_wrapper_many_cameras_vs_oracle(torch, V, T):
+    from eks_amd import synthetic
+    from eks_amd.multiview_pca_smoother import ensemble_kalman_smoother_multi_cam
+    from oracle import eks_oracle as O
+    E = 5
+    st = synthetic.multiview_obs(np.random.default_rng(V), V, E, T, K=1)[:, :, 0, :]  # (E,T,2V)
+    st = st.astype(np.float64)
+    cams = [f"cam{c}" for c in range(V)]
+    markers = [[pd.DataFrame(st[e][:, 2 * c:2 * c + 2], columns=["x", "y"]) for e in range(E)]
+               for c in range(V)]
+    res = ensemble_kalman_smoother_multi_cam(markers, "paw", 0.01, 25, cams)
+    got = np.concatenate([res[c + "_df"].to_numpy()[:, :2] for c in cams], axis=1)
+    ref, _, _ = O.multicam_smooth([st[:, :, 2 * c:2 * c + 2] for c in range(V)], 0.01, 25)
+    assert np.abs(got - ref).max() < 1e-5
+
+
+@pytest.mark.parametrize("r,n,E", [(2, 2, 5), (2, 2, 7), (3, 8, 5), (3, 6, 4)])
+def test_runtime_n_kernel_equals_compiled(torch, r, n, E):
+    from eks_amd import batch, synthetic
+    from oracle import eks_oracle as O
+    rng = np.random.default_rng(r * 100 + n * 10 + E)
+    B, T = 70, 500
+    if r == 2:
+        st = synthetic.singleview_obs(rng, E, T, K=B).transpose(2, 0, 1, 3)
+    else:
+        st = synthetic.multiview_obs(rng, n // 2, E, T, K=B).transpose(2, 0, 1, 3)
+    models = []
+    for b in range(B):
+        preds, ev = O.ensemble_array(st[b].astype(np.float64))
+        p = O.singleview_params(preds, ev, 0.01, 25) if r == 2 else \
+            O.multicam_params(preds, ev, 0.01, 25)
+        models.append(p)
+    stk = lambda k: np.stack([m[k] for m in models])  # noqa: E731
+    params = batch.pack_params(stk("m0"), stk("S0"), stk("A"), stk("Q"), stk("C"), stk("means"))
+    d = batch.make_time_major(st, dtype=np.float32)
+    r1 = batch.smooth(d, params, n=n, r=r, algo=1, flags=0, want_nll=True, want_ms=True,
+                      check=True)
+    r4 = batch.smooth(d, params, n=n, r=r, algo=4, flags=0, want_nll=True, want_ms=True,
+                      check=True)
+    # same update order as the compiled general-C kernel; the ensemble comes
+    # from the runtime-E reduction and the compiler contracts differently, so
+    # the two agree to ~1 ulp rather than bit for bit
+    for k in ("out", "ms", "nll"):
+        np.testing.assert_allclose(r4[k].cpu().numpy(), r1[k].cpu().numpy(), rtol=1e-12,
+                                   atol=1e-10, err_msg=k)
+
+
+def test_runtime_n_nll_and_filter_only(torch):
+    """n = 10 (five cameras): smoothed output, NLL and the filter-only call
+    against the oracle's filtering_pass / compute_nll."""
+    from eks_amd import batch, synthetic
+    from oracle import eks_oracle as O
+    rng = np.random.default_rng(31)
+    B, E, T, n = 3, 5, 800, 10
+    st = synthetic.multiview_obs(rng, 5, E, T, K=B).transpose(2, 0, 1, 3).astype(np.float64)
+    models, refs, nlls = [], [], []
+    for b in range(B):
+        preds, ev = O.ensemble_array(st[b])
+        p = O.multicam_params(preds, ev, 0.01, 25)
+        models.append(p)
+        mf, Vf, S = O.filtering_pass(p["y"], p["m0"], p["S0"], p["C"], np.eye(n), p["A"], p["Q"], ev)
+        ms, _, _ = O.smooth_backward(p["y"], mf, Vf, S, p["A"])
+        refs.append(ms @ p["C"].T + p["means"])
+        nlls.append(O.compute_nll(p["y"], p["m0"], p["S0"], p["C"], p["A"], p["Q"], ev))
+    stk = lambda k: np.stack([m[k] for m in models])  # noqa: E731
+    params = batch.pack_params(stk("m0"), stk("S0"), stk("A"), stk("Q"), stk("C"), stk("means"))
+    d = batch.make_time_major(st, dtype=np.float64)
+    res = batch.smooth(d, params, n=n, r=3, want_nll=True, check=True,
+                       flags=batch.model_flags(stk("A"), stk("C")))
+    assert np.abs(res["out"].cpu().numpy() - np.stack(refs)).max() < 1e-5
+    np.testing.assert_allclose(res["nll"].cpu().numpy(), nlls, rtol=1e-9)
+    np.testing.assert_allclose(batch.nll(d, params, n=n, r=3).cpu().numpy(), nlls, rtol=1e-9)
