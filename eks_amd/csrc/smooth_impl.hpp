@@ -594,7 +594,7 @@ __global__ __launch_bounds__(kBlock) void k_c0_shared(SmoothArgs a, ChunkPlan p)
 }
 
 template <int R, int N, int E, typename T, typename YT, int AI, int CI, bool UNI>
-EKS_DEV __forceinline__ void c1_elem_body(const SmoothArgs &a, const ChunkPlan &p) {
+EKS_DEV void c1_elem_body(const SmoothArgs &a, const ChunkPlan &p) {
   constexpr int D = (E > 0 && E * N <= 16) ? 2 : 1;  // member prefetch distance (steps)
   Lane<UNI> ln;
   const long long B = a.B, TT = a.T;
@@ -662,12 +662,13 @@ __global__ __launch_bounds__(kBlock, W) void k_c1_elem_occ(SmoothArgs a, ChunkPl
   c1_elem_body<R, N, E, T, YT, AI, CI, UNI>(a, p);
 }
 
-// waves per SIMD of k_c1_elem_occ (EKS_C1_WPE: tuning experiments; 0 = the
-// unconstrained kernel)
+// waves per SIMD of k_c1_elem_occ (EKS_C1_WPE=2: tuning experiments; default
+// 0 = the unconstrained kernel.  Config 5, tools/c5_sweep.sh: 2 waves/SIMD
+// (256 VGPRs) ran as fast as 1 (262), 3 (168, spilling) 2.9x slower)
 inline int c1_waves_per_simd() {
   static const int v = [] {
     const char *e = getenv("EKS_C1_WPE");
-    return e ? atoi(e) : 2;
+    return e ? atoi(e) : 0;
   }();
   return v;
 }
@@ -1510,12 +1511,8 @@ int launch_shape(const SmoothArgs &a, int algo, long long L) {
         constexpr int EE = decltype(Ec)::value;
         prof_mark(a.stream, "k_c1_elem");
         if constexpr (R == 3 && is_yev<Tp>::value) {
-          const int w = c1_waves_per_simd();
-          if (w == 2)
+          if (c1_waves_per_simd() == 2)
             hipLaunchKernelGGL((k_c1_elem_occ<R, N, EE, Tp, YT, AI, CI, U, 2>), dim3(gch),
-                               dim3(kBlock), 0, a.stream, a, p);
-          else if (w == 3)
-            hipLaunchKernelGGL((k_c1_elem_occ<R, N, EE, Tp, YT, AI, CI, U, 3>), dim3(gch),
                                dim3(kBlock), 0, a.stream, a, p);
           else
             hipLaunchKernelGGL((k_c1_elem<R, N, EE, Tp, YT, AI, CI, U>), dim3(gch), dim3(kBlock),
