@@ -484,6 +484,58 @@ EKS_DEV void load_state_pl(const double *base, long long plane0, long long B, un
     for (int j = i; j < R; ++j) P[i][j] = P[j][i] = pl(base, plane0 + (k++), B, b);
 }
 
+// Per-trajectory model in plane form (ParamLayout field k of trajectory b in
+// plane k): the streaming passes of algo 3 load the model once per
+// (chunk, trajectory) lane, and the caller's row layout (param_len doubles
+// per trajectory, 160 B at r = n = 2) makes every lane touch two cache lines
+// of which it uses a few fields -- at config 4 about 5 B per keypoint-timestep
+// re-fetched from HBM once the streaming data has evicted them from L2.  In
+// planes a wave's load of one field is one 512-byte segment, and a structure
+// the kernel is compiled for (A = I, C = I) is not read at all: k_model_planes
+// checks it once per trajectory instead.
+template <int R, int N, int AI, int CI>
+EKS_DEV void load_model_pl(const double *base, long long B, unsigned b, bool with_prior,
+                           Model<R, N> &md) {
+  using L = ParamLayout<R, N>;
+  if (with_prior) {
+#pragma unroll
+    for (int i = 0; i < R; ++i) md.m0[i] = pl(base, L::m0 + i, B, b);
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+#pragma unroll
+      for (int j = 0; j < R; ++j) md.S0[i][j] = pl(base, L::S0 + i * R + j, B, b);
+  }
+#pragma unroll
+  for (int i = 0; i < R; ++i)
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      md.A[i][j] = AI == kAId ? (i == j ? 1.0 : 0.0) : pl(base, L::A + i * R + j, B, b);
+      md.Q[i][j] = pl(base, L::Q + i * R + j, B, b);
+    }
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+#pragma unroll
+    for (int j = 0; j < R; ++j)
+      md.C[i][j] = CI == kCId ? (i == j ? 1.0 : 0.0) : pl(base, L::C + i * R + j, B, b);
+#pragma unroll
+  for (int i = 0; i < N; ++i) md.off[i] = pl(base, L::off + i, B, b);
+}
+
+// one thread per trajectory: params rows -> planes, model structure check
+template <int R, int N, int AI, int CI>
+__global__ __launch_bounds__(256) void k_model_planes(const double *params, long long B,
+                                                      double *planes, int32_t *status) {
+  using L = ParamLayout<R, N>;
+  const long long b = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (b >= B) return;
+  const double *pp = params + b * L::len;
+#pragma unroll
+  for (int k = 0; k < L::len; ++k) planes[(long long)k * B + b] = pp[k];
+  Model<R, N> md;
+  md.load(pp, false);
+  if (!md.template valid<AI, CI>()) flag(status, b, EKS_STATUS_BAD_MODEL);
+}
+
 // Stream the chunk's member predictions once: ensemble each step, store the
 // raw average and the variance for K3/K5, and feed the step to `absorb`
 // (the plain filter for chunk 0, the element build otherwise).

@@ -87,7 +87,7 @@ constexpr int fine_len3(int r, int n) { return kNS * sub_len3(r, n); }
 struct Plan3 {
   long long L = 16, NCf = 0, NCc = 0;
   size_t fel_off = 0, cel_off = 0, ccs_off = 0, cmap_off = 0, cms_off = 0, fcs_off = 0,
-         fms_off = 0, nllp_off = 0, total = 0;
+         fms_off = 0, nllp_off = 0, prm_off = 0, total = 0;
 };
 
 inline Plan3 make_plan3(long long B, long long T, int r, int n) {
@@ -112,6 +112,7 @@ inline Plan3 make_plan3(long long B, long long T, int r, int n) {
     p.fms_off = take((size_t)p.NCf * r * Bz * 8);
   }
   p.nllp_off = take((size_t)p.NCf * Bz * 8);
+  p.prm_off = take((size_t)param_len(n, r) * Bz * 8);  // k_model_planes
   p.total = off;
   return p;
 }
@@ -217,9 +218,8 @@ __global__ __launch_bounds__(64 * kWV) EKS_K3E_WPE void k3_elem(SmoothArgs a, Pl
   Elem<R> El;
   El.set_identity();
   if (live) {
-    Model<R, N> md;
-    md.load(a.params + (long long)b * ParamLayout<R, N>::len, f == 0);
-    if (f == 0 && !md.template valid<AI, CI>()) flag(a.status, b, EKS_STATUS_BAD_MODEL);
+    Model<R, N> md;  // structure checked by k_model_planes
+    load_model_pl<R, N, AI, CI>((const double *)(a.ws + p.prm_off), B, b, f == 0, md);
     const long long s = f * p.L, e = min(TT, s + p.L);
     typename SrcOf<E, N, T, D>::type src;
     src.init(a, b);
@@ -657,7 +657,7 @@ __global__ __launch_bounds__(kBlock) void k3_final(SmoothArgs a, Plan3 p) {
   const unsigned b = ln.b;
   const int tid = threadIdx.x;
   Model<R, N> md;
-  md.load(a.params + (long long)b * ParamLayout<R, N>::len, c == 0);
+  load_model_pl<R, N, AI, CI>((const double *)(a.ws + p.prm_off), B, b, c == 0, md);
   const long long s = c * p.L, e = min(TT, s + p.L);
   const bool last = e == TT;
   const int nsub = (int)((e - s + LS - 1) / LS);
@@ -829,7 +829,7 @@ __global__ __launch_bounds__(kBlock) EKS_K3_WPE void k3_final_s(SmoothArgs a, Pl
     b = ln.b;
   }
   Model<R, N> md;
-  md.load(a.params + (long long)b * ParamLayout<R, N>::len, c == 0);
+  load_model_pl<R, N, AI, CI>((const double *)(a.ws + p.prm_off), B, b, c == 0, md);
   const long long s = c * p.L, e = min(TT, s + p.L);
   const bool last = e == TT;
   const int nsub = (int)((e - s + LS - 1) / LS);
@@ -1084,6 +1084,10 @@ int launch_algo3(const SmoothArgs &a) {
     constexpr int EE = decltype(Ec)::value;
     int rc;
     prof_call_begin();
+    prof_mark(a.stream, "k_model_planes");
+    hipLaunchKernelGGL((k_model_planes<R, N, AI, CI>), dim3(grid_for(a.B, 256)), dim3(256), 0, a.stream,
+                       a.params, a.B, (double *)(a.ws + p.prm_off), a.status);
+    if ((rc = check_launch("k_model_planes"))) return rc;
     prof_mark(a.stream, "k3_elem");
     hipLaunchKernelGGL((k3_elem<R, N, EE, Tp, AI, CI>), dim3(g1), dim3(64 * kWV), 0, a.stream, a, p);
     if ((rc = check_launch("k3_elem"))) return rc;
