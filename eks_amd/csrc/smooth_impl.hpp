@@ -545,36 +545,33 @@ EKS_DEV void c1_stream(const SmoothArgs &a, const ChunkPlan &p, long long s, lon
   const long long B = a.B;
   if constexpr (is_yev<T>::value) {
     // the ensemble is already in the caller's planes: stream y / ev
+    // ring loads are unconditional (step index clamped to the chunk's last:
+    // a cache-hit re-read), so they stay in flight: a load under a
+    // lane-divergent `if` is merged into its slot by a copy that waits for it
     constexpr int DY = 2;
     YT yr[DY][N];
     double er[DY][N];
+    auto fetch = [&](int q, long long t) {
 #pragma unroll
-    for (int q = 0; q < DY; ++q)
-      if (s + q < e)
+      for (int j = 0; j < N; ++j) {
+        yr[q][j] = pl((const YT *)p.ysrc, t * N + j, p.yB, p.ylane(b));
+        er[q][j] = pl((const double *)p.evsrc, t * N + j, p.yB, p.ylane(b));
+      }
+    };
 #pragma unroll
-        for (int j = 0; j < N; ++j) {
-          yr[q][j] = pl((const YT *)p.ysrc, (s + q) * N + j, p.yB, p.ylane(b));
-          er[q][j] = pl((const double *)p.evsrc, (s + q) * N + j, p.yB, p.ylane(b));
-        }
+    for (int q = 0; q < DY; ++q) fetch(q, min(s + q, e - 1));
     for (long long t0 = s; t0 < e; t0 += DY) {
 #pragma unroll
       for (int q = 0; q < DY; ++q) {
         const long long t = t0 + q;
-        if (t < e) {
-          double y[N], rv[N];
+        double y[N], rv[N];
 #pragma unroll
-          for (int j = 0; j < N; ++j) {
-            y[j] = (double)yr[q][j] - off[j];
-            rv[j] = er[q][j];
-          }
-          if (t + DY < e)
-#pragma unroll
-            for (int j = 0; j < N; ++j) {
-              yr[q][j] = pl((const YT *)p.ysrc, (t + DY) * N + j, p.yB, p.ylane(b));
-              er[q][j] = pl((const double *)p.evsrc, (t + DY) * N + j, p.yB, p.ylane(b));
-            }
-          absorb(t, y, rv);
+        for (int j = 0; j < N; ++j) {
+          y[j] = (double)yr[q][j] - off[j];
+          rv[j] = er[q][j];
         }
+        fetch(q, min(t + DY, e - 1));
+        if (t < e) absorb(t, y, rv);
       }
     }
     return;
@@ -585,25 +582,24 @@ EKS_DEV void c1_stream(const SmoothArgs &a, const ChunkPlan &p, long long s, lon
   double *evbuf = (double *)(a.ws + p.ev_off);
   const T *ob = (const T *)a.obs + (long long)b * a.sb;
   T ring[D][EE][N];
-  if constexpr (E > 0) {
+  if constexpr (E > 0) {  // unconditional clamped ring loads, as above
 #pragma unroll
-    for (int q = 0; q < D; ++q)
-      if (s + q < e) load_step<E, N, T>(ob + (s + q) * a.st, a.se, a.sj, ring[q]);
+    for (int q = 0; q < D; ++q) load_step<E, N, T>(ob + min(s + q, e - 1) * a.st, a.se, a.sj, ring[q]);
   }
   for (long long t0 = s; t0 < e; t0 += D) {
 #pragma unroll
     for (int q = 0; q < D; ++q) {
       const long long t = t0 + q;
+      T cur[EE][N];
+      if constexpr (E > 0) {
+#pragma unroll
+        for (int u = 0; u < E; ++u)
+#pragma unroll
+          for (int j = 0; j < N; ++j) cur[u][j] = ring[q][u][j];
+        load_step<E, N, T>(ob + min(t + D, e - 1) * a.st, a.se, a.sj, ring[q]);
+      }
       if (t < e) {
         const T *pt = ob + t * a.st;
-        T cur[EE][N];
-        if constexpr (E > 0) {
-#pragma unroll
-          for (int u = 0; u < E; ++u)
-#pragma unroll
-            for (int j = 0; j < N; ++j) cur[u][j] = ring[q][u][j];
-          if (t + D < e) load_step<E, N, T>(pt + D * a.st, a.se, a.sj, ring[q]);
-        }
         double avg[N], rv[N], y[N];
         reduce_step<E, N, T>(cur, pt, a.se, a.sj, a.E, median, avg, rv);
 #pragma unroll
@@ -776,6 +772,37 @@ __global__ __launch_bounds__(64) void k_c2_fscan(SmoothArgs a, ChunkPlan p) {
   if (!ok) flag(a.status, b, EKS_STATUS_SCAN);
 }
 
+// Per-thread runs of the parallel chunk scans: PD element / map loads in
+// flight while one is composed.  The chain is bound by the latency of these
+// loads (K1's / K3's rows live in other XCDs' L2s or HBM, ~1-2 us), not by the
+// compositions, so a depth-1 prefetch pays one load latency per chunk.  Ring
+// loads are unconditional (index clamped into the run: a cache-hit re-read at
+// the tail), so the compiler cannot merge a divergent load into its slot with
+// a copy that waits for it.
+#ifndef EKS_SCAN_PD
+#define EKS_SCAN_PD 1  // config 2 (B = 17, T = 1e5): depth 1 / 2 / 4 -> K2 35 / 39 / 41 us
+#endif
+template <int R>
+constexpr int scan_pd() { return R <= 2 ? EKS_SCAN_PD : 1; }  // r = 3: 27-double elements, 2 would spill at 512 threads
+
+// fn(c, element c) for c = c0 .. c1-1 in order; rows of Elem<R>::len doubles
+template <int R, typename F>
+EKS_DEV void elem_run(const double *rows, long long c0, long long c1, F &&fn) {
+  constexpr int PD = scan_pd<R>();
+  if (c0 >= c1) return;
+  Elem<R> ring[PD];
+#pragma unroll
+  for (int k = 0; k < PD; ++k) ring[k].load(rows + min(c0 + k, c1 - 1) * Elem<R>::len, 1);
+  for (long long c = c0; c < c1; c += PD) {
+#pragma unroll
+    for (int k = 0; k < PD; ++k) {
+      const Elem<R> e = ring[k];
+      ring[k].load(rows + min(c + k + PD, c1 - 1) * Elem<R>::len, 1);
+      if (c + k < c1) fn(c + k, e);
+    }
+  }
+}
+
 // K2, parallel form: one block of W waves per trajectory for many chunks.
 // Thread l owns chunks [l q, (l+1) q): it composes their elements, each wave
 // scans its 64 aggregates (Hillis-Steele, log2 64 = 6 compositions), the
@@ -797,17 +824,11 @@ __global__ __launch_bounds__(64 * W) void k_c2_fscan_w(SmoothArgs a, ChunkPlan p
   bool ok = true;
   Elem<R> agg;
   agg.set_identity();
-  {  // the chain is latency bound: the next element is in flight while one is composed
-    Elem<R> nx;
-    if (c0 < c1) nx.load(elem + (b * NC + c0) * Elem<R>::len, 1);
-    for (long long c = c0; c < c1; ++c) {
-      const Elem<R> e = nx;
-      if (c + 1 < c1) nx.load(elem + (b * NC + c + 1) * Elem<R>::len, 1);
-      Elem<R> t;
-      ok = compose_elem<R>(agg, e, t) && ok;
-      agg = t;
-    }
-  }
+  elem_run<R>(elem + b * NC * Elem<R>::len, c0, c1, [&](long long, const Elem<R> &e) {
+    Elem<R> t;
+    ok = compose_elem<R>(agg, e, t) && ok;
+    agg = t;
+  });
 #pragma unroll
   for (int k = 1; k < 64; k <<= 1) {
     const Elem<R> o = shfl_elem<R, true>(agg, k);
@@ -883,21 +904,15 @@ __global__ __launch_bounds__(64 * W) void k_c2_fscan_w(SmoothArgs a, ChunkPlan p
     }
     double *np_ = (double *)(a.ws + p.nllp_off);
     const bool need = !p.nll_closed;  // the start states feed K3 / K5 (not a closed-form NLL call)
-    Elem<R> nx;
-    if (c < c1) nx.load(elem + (b * NC + c) * Elem<R>::len, 1);
-    for (; c < c1; ++c) {
+    elem_run<R>(elem + b * NC * Elem<R>::len, c, c1, [&](long long c, const Elem<R> &e) {
       if (need) store_state<R>(cst + (c * KS) * B + b, B, m, P);
-      if (c + 1 < c1 || p.nll_closed) {
-        const Elem<R> e = nx;
-        if (c + 1 < c1) nx.load(elem + (b * NC + c + 1) * Elem<R>::len, 1);
-        if (p.nll_closed) {
-          const double sh = elem_nll_share<R>(m, P, e, np_[c * B + b], ok);
-          if (p.nll_fused) nsum += sh;
-          else np_[c * B + b] = sh;
-        }
-        if (c + 1 < c1) ok = compose_state<R>(m, P, e) && ok;
+      if (p.nll_closed) {
+        const double sh = elem_nll_share<R>(m, P, e, np_[c * B + b], ok);
+        if (p.nll_fused) nsum += sh;
+        else np_[c * B + b] = sh;
       }
-    }
+      if (c + 1 < c1) ok = compose_state<R>(m, P, e) && ok;
+    });
     if (tid == 0 && p.nll_fused) nsum += np_[b];  // chunk 0's share: the plain filter's (K1)
   }
   if (p.nll_fused) {  // the NLL sum: per thread in chunk order, then the block (fixed order)
@@ -978,17 +993,25 @@ __global__ __launch_bounds__(64 * W) void k_c4_bscan_w(SmoothArgs a, ChunkPlan p
     return f;
   };
   auto map_of = [&](long long c) { return load_map(bw + (b * NC + c) * (R * R + R)); };
+  // fn(c, map c) for c = c1-1 down to c0, PD maps in flight (see elem_run)
+  auto map_run = [&](auto &&fn) {
+    constexpr int PD = 2 * scan_pd<R>();
+    if (c0 >= c1) return;
+    Affine<R> ring[PD];
+#pragma unroll
+    for (int k = 0; k < PD; ++k) ring[k] = map_of(max(c1 - 1 - k, c0));
+    for (long long c = c1 - 1; c >= c0; c -= PD) {
+#pragma unroll
+      for (int k = 0; k < PD; ++k) {
+        const Affine<R> f = ring[k];
+        ring[k] = map_of(max(c - k - PD, c0));
+        if (c - k >= c0) fn(c - k, f);
+      }
+    }
+  };
   Affine<R> F;
   F.set_identity();
-  {  // latency bound: the next map is in flight while one is composed
-    Affine<R> nx;
-    if (c1 > c0) nx = map_of(c1 - 1);
-    for (long long c = c1 - 1; c >= c0; --c) {
-      const Affine<R> f = nx;
-      if (c - 1 >= c0) nx = map_of(c - 1);
-      F = f.after(F);
-    }
-  }
+  map_run([&](long long, const Affine<R> &f) { F = f.after(F); });
 #pragma unroll
   for (int k = 1; k < 64; k <<= 1) {
     const Affine<R> o = F.shfl_down(k);
@@ -1023,15 +1046,11 @@ __global__ __launch_bounds__(64 * W) void k_c4_bscan_w(SmoothArgs a, ChunkPlan p
       for (int k = 0; k < R; ++k) t = fma(X.G[i][k], a.seg_in[b * R + k], t);
     ms[i] = t;
   }
-  Affine<R> nxm;
-  if (c1 > c0) nxm = map_of(c1 - 1);
-  for (long long c = c1 - 1; c >= c0; --c) {
+  map_run([&](long long c, const Affine<R> &f) {
     if (c + 1 < NC || a.seg_in) {
 #pragma unroll
       for (int i = 0; i < R; ++i) msend[(c * R + i) * B + b] = ms[i];
     }
-    const Affine<R> f = nxm;
-    if (c - 1 >= c0) nxm = map_of(c - 1);
     double nx[R];
 #pragma unroll
     for (int i = 0; i < R; ++i) {
@@ -1042,7 +1061,7 @@ __global__ __launch_bounds__(64 * W) void k_c4_bscan_w(SmoothArgs a, ChunkPlan p
     }
 #pragma unroll
     for (int i = 0; i < R; ++i) ms[i] = nx[i];
-  }
+  });
   if (a.nll) {
     const double *np_ = (const double *)(a.ws + p.nllp_off);
     double s = 0.0;
@@ -1261,24 +1280,23 @@ __global__ __launch_bounds__(kBlock) void k_c3_rerun(SmoothArgs a, ChunkPlan p) 
   NllAcc acc;
   YT yr[D][N];
   double er[D][N];
+  // unconditional ring loads, step clamped to the chunk's last (see c1_stream)
 #pragma unroll
-  for (int q = 0; q < D; ++q)
-    if (s + q < e) load_yev<N, YT>(ybuf, evbuf, s + q, p.yB, p.ylane(b), yr[q], er[q]);
+  for (int q = 0; q < D; ++q) load_yev<N, YT>(ybuf, evbuf, min(s + q, e - 1), p.yB, p.ylane(b), yr[q], er[q]);
   long long k = 0;
   for (long long t0 = s; t0 < e; t0 += LS, ++k) {
     if (p.smooth) store_state_pl<R>(ckpt, (c * p.NSUB + k) * KS, B, b, m, P);  // state before t0
 #pragma unroll
     for (int q = 0; q < LS; ++q) {
       const long long t = t0 + q;
-      if (t < e) {
-        double y[N], rv[N];
+      double y[N], rv[N];
 #pragma unroll
-        for (int j = 0; j < N; ++j) {
-          y[j] = (double)yr[q % D][j] - md.off[j];
-          rv[j] = er[q % D][j];
-        }
-        if (t + D < e)
-          load_yev<N, YT>(ybuf, evbuf, t + D, p.yB, p.ylane(b), yr[q % D], er[q % D]);
+      for (int j = 0; j < N; ++j) {
+        y[j] = (double)yr[q % D][j] - md.off[j];
+        rv[j] = er[q % D][j];
+      }
+      load_yev<N, YT>(ybuf, evbuf, min(t + D, e - 1), p.yB, p.ylane(b), yr[q % D], er[q % D]);
+      if (t < e) {
         if (t + a.t_base > 0) kf_predict<R, AI>(m, P, md.A, md.Q);
         kf_update<R, N, CI>(m, P, md.C, y, rv, acc, ok);
         if (!p.smooth) continue;
@@ -1433,9 +1451,10 @@ __global__ __launch_bounds__(kBlock) void k_c5_final(SmoothArgs a, ChunkPlan p) 
     load_state_pl<R>(ckpt, (c * p.NSUB + k) * KS, B, b, m, P);
     YT yr[LS][N];
     double er[LS][N];
+    // unconditional loads (step clamped to the chunk's last): a divergent
+    // `if` around each would serialise them (see c1_stream)
 #pragma unroll
-    for (int j = 0; j < LS; ++j)
-      if (t0 + j < e) load_yev<N, YT>(ybuf, evbuf, t0 + j, p.yB, p.ylane(b), yr[j], er[j]);
+    for (int j = 0; j < LS; ++j) load_yev<N, YT>(ybuf, evbuf, min(t0 + j, e - 1), p.yB, p.ylane(b), yr[j], er[j]);
     double Jr[LS][R][R], dr[LS][R];
 #pragma unroll
     for (int j = 0; j < LS; ++j) {
