@@ -97,7 +97,11 @@ inline int scan_waves(long long NC) {
     return e ? atoi(e) : 0;
   }();
   if (forced == 1 || forced == 4 || forced == 8) return forced;
-  return NC > 512 ? 8 : (NC > 256 ? 4 : 1);
+  // 4 waves (one per SIMD) beat 8 at configs 2 / 3 / 5 (NC = 3 125 / 1 563 /
+  // 17 858: 0.147 / 0.301 / 2.92 -> 0.142 / 0.295 / 2.88 ms per step,
+  // tools/scan_waves_sweep.sh): the waves of one trajectory's block share the
+  // FP64 pipes of one CU, and W = 4 halves the serial cross-wave LDS prefix
+  return NC > 256 ? 4 : 1;
 }
 
 inline long long target_lanes() {
@@ -641,9 +645,20 @@ __global__ __launch_bounds__(kBlock) void k_c0_shared(SmoothArgs a, ChunkPlan p)
   }
 }
 
+// few-trajectory prefetch distances of K1 / K3 (config 2: 2 / 4 / 8 steps all
+// within 2 %, tools/c2_dsweep.sh -- these lanes are bound by the per-step FP64
+// dependency chain, not by the load latency)
+#ifndef EKS_C1_DNU
+#define EKS_C1_DNU 2
+#endif
+#ifndef EKS_C3_DNU
+#define EKS_C3_DNU 2
+#endif
 template <int R, int N, int E, typename T, typename YT, int AI, int CI, bool UNI>
 EKS_DEV void c1_elem_body(const SmoothArgs &a, const ChunkPlan &p) {
-  constexpr int D = (E > 0 && E * N <= 16) ? 2 : 1;  // member prefetch distance (steps)
+  // member prefetch distance (steps); few-trajectory lanes (!UNI: < 1 wave per
+  // SIMD, nothing else to hide the HBM latency behind) keep more in flight
+  constexpr int D = (E > 0 && E * N <= 16) ? (UNI ? 2 : EKS_C1_DNU) : 1;
   Lane<UNI> ln;
   const long long B = a.B, TT = a.T;
   if (!ln.init(B, p.NC)) return;
@@ -1253,7 +1268,7 @@ template <int R, int N, typename YT, int AI, int CI, int LS, bool UNI>
 __global__ __launch_bounds__(kBlock) void k_c3_rerun(SmoothArgs a, ChunkPlan p) {
   // y / ev prefetch distance (steps; divides LS): 2 keeps the (2, 2) kernel at
   // 3 waves/SIMD (160 VGPRs), measured 3 % faster than 4 (174 VGPRs, 2 waves)
-  constexpr int D = (R <= 2 && N <= 2) ? 2 : (LS < 4 ? LS : 4);
+  constexpr int D = (R <= 2 && N <= 2) ? (UNI ? 2 : EKS_C3_DNU) : (LS < 4 ? LS : 4);
   static_assert(LS % D == 0, "prefetch distance must divide the checkpoint interval");
   Lane<UNI> ln;
   const long long B = a.B, TT = a.T;
