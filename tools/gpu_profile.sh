@@ -21,7 +21,7 @@ step() {  # name, timeout, rocprof args...
   done
   return $rc
 }
-RX='k_c[0-9]|k3_|k_smooth_seq|k_fit'
+RX='k_c[0-9]|k3_|k_model|k_smooth_seq|k_fit'
 step trace 600 --kernel-trace --stats || exit $?
 STEPS=2 step pmc_fetch 600 --kernel-include-regex "$RX" --pmc FETCH_SIZE || exit $?
 STEPS=2 step pmc_write 600 --kernel-include-regex "$RX" --pmc WRITE_SIZE || exit $?

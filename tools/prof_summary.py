@@ -64,7 +64,7 @@ def main(src: str, dst: str, key: str | None = None):
         summary["kernels"][k] = d
         # the eks_smooth pipeline on member predictions (not the fit, not the
         # hand-off variant of K1 the bench's end-to-end loop runs)
-        if ("k_c" in k or "k3_" in k or "k_smooth_seq" in k) and "YevIn" not in k:
+        if ("k_c" in k or "k3_" in k or "k_model" in k or "k_smooth_seq" in k) and "YevIn" not in k:
             tot_bytes += b
             tot_ms += d.get("avg_ms", 0.0)
     summary["per_call"] = {"hbm_bytes": tot_bytes, "kernel_ms": tot_ms,
