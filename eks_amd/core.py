@@ -60,6 +60,44 @@ def ensemble_array(stack, mode: str = "median"):
     return preds.cpu().numpy(), var.cpu().numpy()
 
 
+def ensemble_handoff(stack, mode: str = "median"):
+    """(E, T, n) member array -> (yev, preds (T, n), vars (T, n)).
+
+    Like ``ensemble_array``, but the device ensemble is written straight into
+    the y / ev hand-off planes that ``batch.smooth`` accepts in place of the
+    members (include/eks_hip.h eks_yev_bytes; for one trajectory the y and ev
+    planes are the (T, n) arrays, ev starting at the next 256-byte boundary).
+    The per-keypoint wrappers fit their model on the host copies and smooth
+    from the planes: the members are uploaded and reduced once, not twice."""
+    from .batch import Yev
+    torch = _lib.require_gpu()
+    if mode == "median":
+        m = _lib.EKS_MEDIAN
+    elif mode == "mean":
+        m = _lib.EKS_MEAN
+    else:
+        raise ValueError(f"{mode} averaging not supported")
+    stack = np.asarray(stack, dtype=np.float64)
+    E, T, n = stack.shape
+    d = _to_dev(stack, torch)
+    lib = _lib.load()
+    code = lib.eks_yev_dtype(_lib.EKS_F64, E, m)
+    if code != _lib.EKS_YEV64:
+        raise RuntimeError(f"eks_yev_dtype(F64) = {code}, expected EKS_YEV64")
+    nbytes = lib.eks_yev_bytes(1, T, n, _lib.EKS_F64, E, m)
+    ev_off = (T * n * 8 + 255) // 256 * 256
+    buf = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    if nbytes < ev_off + T * n * 8:
+        raise RuntimeError("eks_yev_bytes smaller than the (T, n) y / ev planes")
+    _lib.check(lib.eks_ensemble(d.data_ptr(), _lib.EKS_F64, 1, T, E, n, 0, n, T * n, 1, m,
+                                buf.data_ptr(), buf.data_ptr() + ev_off, _lib.stream_ptr()),
+               "eks_ensemble")
+    planes = buf[:ev_off + T * n * 8]
+    preds = planes[:T * n * 8].view(torch.float64).reshape(T, n).cpu().numpy()
+    var = planes[ev_off:].view(torch.float64).reshape(T, n).cpu().numpy()
+    return Yev(buf, 1, T, E, n, code, mode), preds, var
+
+
 def ensemble(markers_list, keys, mode: str = "median"):
     """eks/ensemble_kalman.py:4-57, same 6-tuple:
     (ensemble_preds (T,n), ensemble_vars (T,n), ensemble_stacks (E,T,n),

@@ -7,9 +7,11 @@
     eks_opti_smoother_pupil              eks/pupil_smoother.py:227-320
 
 Flow for one keypoint: member DataFrames -> (E, T, n) array -> GPU ensemble
-(eks_ensemble) -> host model fit (eks_amd.fit) -> GPU fused smoother
-(eks_smooth: ensemble, forward, backward, projection) -> DataFrames in the
-reference's output format.  No step of the smoother runs on the CPU.
+(eks_ensemble, written as the y / ev hand-off planes) -> host model fit
+(eks_amd.fit, on the planes' host copies) -> GPU fused smoother from the
+planes (eks_smooth: forward, backward, projection) -> DataFrames in the
+reference's output format.  The members are uploaded and reduced once; no
+step of the smoother runs on the CPU.
 """
 from __future__ import annotations
 
@@ -22,13 +24,20 @@ from .utils import TRACKER, make_dlc_pandas_index
 
 
 def _run_fused(stack: np.ndarray, model: dict, mode: str = "median", want_ms=False,
-               want_nll=False):
-    """stack (E, T, n) float64 host array + model -> out (T, n), ms, nll."""
+               want_nll=False, yev=None):
+    """stack (E, T, n) float64 host array + model -> out (T, n), ms, nll.
+    With ``yev`` (core.ensemble_handoff's planes of the same stack) the
+    smoother reads the planes instead of uploading and reducing the members
+    again -- except on the runtime-n kernel (algo 4: shapes without compiled
+    kernels), which reads member predictions only."""
     torch = _lib.require_gpu()
     E, T, n = stack.shape
     r = len(model["m0"])
-    obs = torch.from_numpy(np.ascontiguousarray(stack, dtype=np.float64)).to("cuda")
-    obs = obs.permute(1, 0, 2).unsqueeze(0)  # (1, T, E, n) view, no copy
+    if yev is not None and _lib.load().eks_smooth_algo(1, T, n, r, E, 0) != 4:
+        obs = yev
+    else:
+        obs = torch.from_numpy(np.ascontiguousarray(stack, dtype=np.float64)).to("cuda")
+        obs = obs.permute(1, 0, 2).unsqueeze(0)  # (1, T, E, n) view, no copy
     params = batch.pack_params(model["m0"], model["S0"], model["A"], model["Q"], model["C"],
                                model["offset"])
     res = batch.smooth(obs, params, n=n, r=r, mode=mode, want_ms=want_ms, want_nll=want_nll,
@@ -56,9 +65,9 @@ def ensemble_kalman_smoother_multi_cam(markers_list_cameras, keypoint_ensemble, 
     cols = [np.stack([np.asarray(markers_list_cameras[c][e].to_numpy()[:, :2], dtype=np.float64)
                       for e in range(n_models)]) for c in range(V)]  # V x (E, T, 2)
     stack = np.concatenate(cols, axis=2)  # (E, T, 2V), camera-major columns
-    preds, ev = core.ensemble_array(stack)
+    yev, preds, ev = core.ensemble_handoff(stack)
     model = fit.multicam_model(preds, ev, smooth_param, quantile_keep_pca)
-    out, _, _ = _run_fused(stack, model)
+    out, _, _ = _run_fused(stack, model, yev=yev)
     pdindex = make_dlc_pandas_index([keypoint_ensemble])
     dfs = {}
     nan = np.full(out.shape[0], np.nan)
@@ -76,9 +85,9 @@ def ensemble_kalman_smoother_pupil(markers_list, keypoint_names, tracker_name,
     left (NaN likelihood), 'latents_df': diameter, com_x, com_y}."""
     stack = np.stack([np.stack([np.asarray(df[k], dtype=np.float64) for k in fit.PUPIL_KEYS], 1)
                       for df in markers_list])  # (E, T, 8)
-    preds, _ = core.ensemble_array(stack)
+    yev, preds, _ = core.ensemble_handoff(stack)
     model = fit.pupil_model(preds, state_transition_matrix)
-    out, ms, _ = _run_fused(stack, model, want_ms=True)
+    out, ms, _ = _run_fused(stack, model, want_ms=True, yev=yev)
     by_key = {k: out[:, j] for j, k in enumerate(fit.PUPIL_KEYS)}
     nan = np.full(out.shape[0], np.nan)
     cols = []
@@ -136,9 +145,9 @@ def ensemble_kalman_smoother_single_view(markers_list, keypoint_ensemble, smooth
     keys = [f"{keypoint_ensemble}_x", f"{keypoint_ensemble}_y"]
     stack = np.stack([np.stack([np.asarray(df[k], dtype=np.float64) for k in keys], 1)
                       for df in markers_list])  # (E, T, 2)
-    preds, ev = core.ensemble_array(stack, ensembling_mode)
+    yev, preds, ev = core.ensemble_handoff(stack, ensembling_mode)
     model = fit.singleview_model(preds, ev, smooth_param, quantile_keep_pca)
-    out, _, nll = _run_fused(stack, model, mode=ensembling_mode, want_nll=True)
+    out, _, nll = _run_fused(stack, model, mode=ensembling_mode, want_nll=True, yev=yev)
     nan = np.full(out.shape[0], np.nan)
     df = pd.DataFrame(np.stack([out[:, 0], out[:, 1], nan], 1),
                       columns=make_dlc_pandas_index([keypoint_ensemble]))
