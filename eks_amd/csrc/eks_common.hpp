@@ -26,6 +26,7 @@ void clear_err();
 void prof_mark(hipStream_t s, const char *next_kernel);
 void prof_call_begin();
 void prof_call_end(hipStream_t s);
+void prof_suspend(bool on);
 
 template <int R>
 EKS_DEV void load_vec(const double *p, double (&v)[R]) {

@@ -61,16 +61,21 @@ struct Prof {
   std::vector<std::string> names;  // [call * kMarks + mark]: kernel launched after the mark
 };
 static thread_local Prof g_prof;
+// > 0 while a launcher times a multi-stream call as one interval (its inner
+// launchers' marks would interleave across streams)
+static thread_local int g_prof_suspend = 0;
+
+void prof_suspend(bool on) { g_prof_suspend += on ? 1 : -1; }
 
 void prof_call_begin() {
-  if (!g_prof.on) return;
+  if (!g_prof.on || g_prof_suspend) return;
   if (g_prof.call + 1 >= g_prof.max_calls) return;
   ++g_prof.call;
   g_prof.mark = 0;
 }
 
 void prof_mark(hipStream_t s, const char *next_kernel) {
-  if (!g_prof.on || g_prof.call < 0 || g_prof.call >= g_prof.max_calls) return;
+  if (!g_prof.on || g_prof_suspend || g_prof.call < 0 || g_prof.call >= g_prof.max_calls) return;
   if (g_prof.mark >= Prof::kMarks) return;
   hipEventRecord(g_prof.ev[g_prof.call * Prof::kMarks + g_prof.mark], s);
   g_prof.names[g_prof.call * Prof::kMarks + g_prof.mark] = next_kernel ? next_kernel : "";

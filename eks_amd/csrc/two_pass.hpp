@@ -1068,7 +1068,7 @@ __global__ __launch_bounds__(64) void k3_nll(SmoothArgs a, Plan3 p) {
 
 // host: the four (five with NLL) launches of one algo-3 call
 template <int R, int N, int AI, int CI>
-int launch_algo3(const SmoothArgs &a) {
+int launch_algo3(const SmoothArgs &a, hipEvent_t after_elem = nullptr, hipStream_t cont = nullptr) {
   constexpr int LS = sub_len_c(R, N);
   const Plan3 p = make_plan3(a.B, a.T, R, N);
   const bool yev = a.dtype == EKS_YEV32 || a.dtype == EKS_YEV64;
@@ -1091,33 +1091,39 @@ int launch_algo3(const SmoothArgs &a) {
     prof_mark(a.stream, "k3_elem");
     hipLaunchKernelGGL((k3_elem<R, N, EE, Tp, AI, CI>), dim3(g1), dim3(64 * kWV), 0, a.stream, a, p);
     if ((rc = check_launch("k3_elem"))) return rc;
-    prof_mark(a.stream, "k3_coarse");
+    if (after_elem && hipEventRecord(after_elem, a.stream) != hipSuccess)
+      return set_err(EKS_ERR_HIP, "eks_smooth algo 3: hipEventRecord failed");
+    // (split calls) the rest of this half's chain continues on `cont`
+    const hipStream_t sc = cont ? cont : a.stream;
+    if (cont && hipStreamWaitEvent(cont, after_elem, 0) != hipSuccess)
+      return set_err(EKS_ERR_HIP, "eks_smooth algo 3: hipStreamWaitEvent failed");
+    prof_mark(sc, "k3_coarse");
     switch (coarse_subparts(a.B)) {
-      case 8: hipLaunchKernelGGL((k3_coarse<R, 8>), dim3(grid_for(a.B, 8)), dim3(64 * kNP), 0, a.stream, a, p); break;
-      case 4: hipLaunchKernelGGL((k3_coarse<R, 4>), dim3(grid_for(a.B, 16)), dim3(64 * kNP), 0, a.stream, a, p); break;
-      case 2: hipLaunchKernelGGL((k3_coarse<R, 2>), dim3(grid_for(a.B, 32)), dim3(64 * kNP), 0, a.stream, a, p); break;
-      default: hipLaunchKernelGGL((k3_coarse<R, 1>), dim3(grid_for(a.B, 64)), dim3(64 * kNP), 0, a.stream, a, p);
+      case 8: hipLaunchKernelGGL((k3_coarse<R, 8>), dim3(grid_for(a.B, 8)), dim3(64 * kNP), 0, sc, a, p); break;
+      case 4: hipLaunchKernelGGL((k3_coarse<R, 4>), dim3(grid_for(a.B, 16)), dim3(64 * kNP), 0, sc, a, p); break;
+      case 2: hipLaunchKernelGGL((k3_coarse<R, 2>), dim3(grid_for(a.B, 32)), dim3(64 * kNP), 0, sc, a, p); break;
+      default: hipLaunchKernelGGL((k3_coarse<R, 1>), dim3(grid_for(a.B, 64)), dim3(64 * kNP), 0, sc, a, p);
     }
     if ((rc = check_launch("k3_coarse"))) return rc;
 #if EKS_K3_MERGED
-    prof_mark(a.stream, "k3_final");
+    prof_mark(sc, "k3_final");
     hipLaunchKernelGGL((k3_final_s<R, N, EE, Tp, YT, AI, CI, LS, true>), dim3(g1), dim3(kBlock), 0,
-                       a.stream, a, p);
+                       sc, a, p);
 #else
-    prof_mark(a.stream, "k3_fine");
-    hipLaunchKernelGGL((k3_fine<R>), dim3(g3), dim3(kBlock), 0, a.stream, a, p);
+    prof_mark(sc, "k3_fine");
+    hipLaunchKernelGGL((k3_fine<R>), dim3(g3), dim3(kBlock), 0, sc, a, p);
     if ((rc = check_launch("k3_fine"))) return rc;
-    prof_mark(a.stream, "k3_final");
+    prof_mark(sc, "k3_final");
     hipLaunchKernelGGL((k3_final_s<R, N, EE, Tp, YT, AI, CI, LS, false>), dim3(g4), dim3(kBlock), 0,
-                       a.stream, a, p);
+                       sc, a, p);
 #endif
     if ((rc = check_launch("k3_final"))) return rc;
     if (a.nll) {
-      prof_mark(a.stream, "k3_nll");
-      hipLaunchKernelGGL((k3_nll<R>), dim3((unsigned)a.B), dim3(64), 0, a.stream, a, p);
+      prof_mark(sc, "k3_nll");
+      hipLaunchKernelGGL((k3_nll<R>), dim3((unsigned)a.B), dim3(64), 0, sc, a, p);
       if ((rc = check_launch("k3_nll"))) return rc;
     }
-    prof_call_end(a.stream);
+    prof_call_end(sc);
     return 0;
   };
   if (yev) {
@@ -1134,4 +1140,103 @@ int launch_algo3(const SmoothArgs &a) {
   };
   if (y32) return by_e(float{}, float{});
   return f32 ? by_e(float{}, double{}) : by_e(double{}, double{});
+}
+
+// ---------------------------------------------------------------------------
+// Two half-batches on two streams (EKS_A3_SPLIT = 1 / 2; off by default:
+// measured no faster).  k3_coarse holds a whole CU per block (242 VGPRs x 8
+// waves, 83 KB LDS) for a latency-bound chain, and k3_fine is short; in one
+// stream nothing else runs beside them (15 % of the config-4 step).  Split
+// into halves A and B (A = whole 64-trajectory groups): mode 1 starts B's
+// chain on a side stream when A's k3_elem is done; mode 2 continues A's
+// scans + final pass on a high-priority side stream while B's k3_elem
+// follows on the caller's stream.  Either way one half's member pass streams
+// beside the other half's scans; the caller's stream then joins the side
+// stream.  Each half is an ordinary algo-3 call on its own workspace range
+// (planes pitched by the half's B), so results are bit-identical to two
+// separate calls on the halves (and to the one-piece call whenever the
+// half's coarse sub-part count S equals the whole's, e.g. config 4's
+// 17 408 -> 2 x 8 704, S = 1).  Measured at config 4 (profiles/r02/split):
+// the kernels do overlap (A's k3_coarse runs beside B's k3_elem) but the
+// coarse scan is starved (0.94 instead of 0.25 ms) while k3_elem keeps its
+// 0.80 ms: the step is bound by its total HBM traffic (22.2 GB at 5.3 TB/s),
+// which overlap does not reduce (4.21 / 4.21 / 4.22 ms for one stream /
+// mode 1 / mode 2).
+// ---------------------------------------------------------------------------
+constexpr long long kSplitMinB = 8192;
+
+inline int a3_split_mode() {  // read per call (tests switch it)
+  const char *e = getenv("EKS_A3_SPLIT");
+  return e ? atoi(e) : 0;
+}
+
+struct SplitRes {  // per device: the side stream and the fork / join events
+  hipStream_t side = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+};
+
+inline SplitRes *split_res() {
+  static SplitRes res[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  SplitRes &r = res[dev];
+  if (!r.side) {
+    int least = 0, greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) greatest = 0;
+    if (hipStreamCreateWithPriority(&r.side, hipStreamNonBlocking, greatest) != hipSuccess ||
+        hipEventCreateWithFlags(&r.fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&r.join, hipEventDisableTiming) != hipSuccess) {
+      r.side = nullptr;
+      return nullptr;
+    }
+  }
+  return &r;
+}
+
+template <int R, int N, int AI, int CI>
+int launch_algo3_split(const SmoothArgs &a) {
+  const int mode = a3_split_mode();
+  const bool members = a.dtype == EKS_F32 || a.dtype == EKS_F64;
+  const long long b0 = (a.B / 2 + 63) / 64 * 64;  // half A: whole 64-trajectory groups
+  bool go = members && a.phase == 0 && b0 < a.B && mode > 0 && a.B >= kSplitMinB;
+  SmoothArgs A = a, Bh = a;
+  if (go) {
+    A.B = b0;
+    A.ws_bytes = align256(make_plan3(b0, a.T, R, N).total);
+    Bh.B = a.B - b0;
+    Bh.ws = a.ws + A.ws_bytes;
+    Bh.ws_bytes = make_plan3(Bh.B, a.T, R, N).total;
+    go = A.ws_bytes + Bh.ws_bytes <= a.ws_bytes;
+  }
+  SplitRes *sr = go ? split_res() : nullptr;
+  if (!sr) return launch_algo3<R, N, AI, CI>(a);
+  const size_t esz = a.dtype == EKS_F32 ? 4 : 8;
+  Bh.obs = (const char *)a.obs + (size_t)(b0 * a.sb) * esz;
+  Bh.params = a.params + b0 * ParamLayout<R, N>::len;
+  Bh.out = a.out + b0 * a.ob;
+  Bh.ms = a.ms ? a.ms + b0 * a.T * R : nullptr;
+  Bh.nll = a.nll ? a.nll + b0 : nullptr;
+  Bh.status = a.status ? a.status + b0 : nullptr;
+  prof_call_begin();
+  prof_mark(a.stream, "k3_split");
+  prof_suspend(true);
+  int rc;
+  if (mode == 1) {  // B's whole chain on the side stream after A's k3_elem
+    Bh.stream = sr->side;
+    rc = launch_algo3<R, N, AI, CI>(A, sr->fork);
+    if (!rc && hipStreamWaitEvent(sr->side, sr->fork, 0) != hipSuccess)
+      rc = set_err(EKS_ERR_HIP, "eks_smooth algo 3 split: hipStreamWaitEvent failed");
+    if (!rc) rc = launch_algo3<R, N, AI, CI>(Bh);
+  } else {  // A's scans + final pass on the (high-priority) side stream, B on the caller's
+    Bh.stream = a.stream;
+    rc = launch_algo3<R, N, AI, CI>(A, sr->fork, sr->side);
+    if (!rc) rc = launch_algo3<R, N, AI, CI>(Bh);
+  }
+  // join even after a failed half so the side stream never outlives the call
+  if (hipEventRecord(sr->join, sr->side) != hipSuccess ||
+      hipStreamWaitEvent(a.stream, sr->join, 0) != hipSuccess)
+    rc = rc ? rc : set_err(EKS_ERR_HIP, "eks_smooth algo 3 split: join failed");
+  prof_suspend(false);
+  prof_call_end(a.stream);
+  return rc;
 }

@@ -811,3 +811,34 @@ def test_filter_only_closed_form_nll(torch, kind, B, T):
     o2 = batch.smooth(one, p1, n=n, r=r, algo=2, flags=flags)["out"]
     o1 = batch.smooth(one, p1, n=n, r=r, algo=1, flags=flags)["out"]
     assert float((o2 - o1).abs().max()) < 1e-8
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+def test_algo3_split_streams(torch, mode, monkeypatch):
+    """EKS_A3_SPLIT = 1 / 2 runs algo 3 from 8 192 trajectories as two
+    half-batches on two streams (two_pass.hpp launch_algo3_split; half A =
+    whole 64-trajectory groups).  The split call must equal two separate
+    calls on the halves bit for bit (each below the split threshold, so one
+    stream each), and the sequential recursion (algo 1) to < 1e-8 px / NLL
+    rtol 1e-10, ragged last group included."""
+    from eks_amd import _lib, batch, synthetic
+    monkeypatch.setenv("EKS_A3_SPLIT", str(mode))
+    rng = np.random.default_rng(22)
+    B, T, E = 8200, 300, 5
+    b0 = (B // 2 + 63) // 64 * 64
+    st = synthetic.singleview_obs(rng, E, T, K=B).transpose(2, 0, 1, 3).astype(np.float32)
+    d = batch.make_time_major(st, dtype=np.float32)               # (B, T, E, 2) view
+    params = batch.fit(d, kind="singleview", n=2, r=2, smooth_param=0.01, quantile_keep=25)[0]
+    flags = _lib.EKS_MODEL_A_IDENTITY | _lib.EKS_MODEL_C_IDENTITY
+    full = batch.smooth(d, params, n=2, r=2, algo=3, flags=flags, want_ms=True, want_nll=True)
+    assert (full["status"] == 0).all()
+    for lo, hi in ((0, b0), (b0, B)):
+        part = batch.smooth(d[lo:hi], params[lo:hi].contiguous(), n=2, r=2, algo=3, flags=flags,
+                            want_ms=True, want_nll=True)
+        assert torch.equal(part["out"], full["out"][lo:hi]), (lo, hi)
+        assert torch.equal(part["ms"], full["ms"][lo:hi]), (lo, hi)
+        assert torch.equal(part["nll"], full["nll"][lo:hi]), (lo, hi)
+        assert torch.equal(part["status"], full["status"][lo:hi]), (lo, hi)
+    ref = batch.smooth(d, params, n=2, r=2, algo=1, flags=flags, want_nll=True)
+    assert float((full["out"] - ref["out"]).abs().max()) < 1e-8
+    np.testing.assert_allclose(full["nll"].cpu().numpy(), ref["nll"].cpu().numpy(), rtol=1e-10)
