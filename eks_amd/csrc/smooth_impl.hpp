@@ -46,6 +46,19 @@
 
 namespace eks {
 
+// algo 3's member passes stream ~7 GB (config 4) that no cache holds
+// between the two passes: member loads and output stores are non-temporal
+// there (config 4: k3_elem 1.67 -> 1.62, k3_final 1.93 -> 1.87 ms,
+// profiles/r02/nt).  Algo 2 keeps cached loads: its few-trajectory shapes
+// re-read members from the Infinity Cache (config 2 K1 0.046 -> 0.061 ms
+// with non-temporal loads).  0 turns them off (tuning builds).
+#ifndef EKS_NT_LOAD
+#define EKS_NT_LOAD 1
+#endif
+#ifndef EKS_NT_OUT
+#define EKS_NT_OUT 1
+#endif
+
 struct SmoothArgs {
   const void *obs;
   int dtype;

@@ -132,7 +132,17 @@ struct MemberRing {
     sj = a.sj;
     median = a.median != 0;
   }
-  EKS_DEV void fetch(int slot, long long t) { load_step<E, N, T>(ob + t * st, se, sj, v[slot]); }
+  EKS_DEV void fetch(int slot, long long t) {
+#if EKS_NT_LOAD
+    const T *p = ob + t * st;
+#pragma unroll
+    for (int e = 0; e < E; ++e)
+#pragma unroll
+      for (int j = 0; j < N; ++j) v[slot][e][j] = __builtin_nontemporal_load(p + e * se + j * sj);
+#else
+    load_step<E, N, T>(ob + t * st, se, sj, v[slot]);
+#endif
+  }
   EKS_DEV void get(int slot, double (&avg)[N], double (&rv)[N]) const {
 #pragma unroll
     for (int j = 0; j < N; ++j) {
@@ -760,7 +770,12 @@ __global__ __launch_bounds__(kBlock) void k3_final(SmoothArgs a, Plan3 p) {
                 cm[j] = u + md.off[j];
               }
             }
-            *(double2 *)(outb + t * a.ot) = make_double2(cm[0], cm[1]);
+    #if EKS_NT_OUT  // streaming (non-temporal) output stores (smooth_impl.hpp)
+        __builtin_nontemporal_store(cm[0], outb + t * a.ot);
+        __builtin_nontemporal_store(cm[1], outb + t * a.ot + 1);
+#else
+        *(double2 *)(outb + t * a.ot) = make_double2(cm[0], cm[1]);
+#endif
           } else {
             project_store<R, N, CI>(outb + t * a.ot, a.oj, md.C, ms, md.off);
           }
@@ -993,7 +1008,12 @@ __global__ __launch_bounds__(kBlock) EKS_K3_WPE void k3_final_s(SmoothArgs a, Pl
             cm[j] = u + md.off[j];
           }
         }
+#if EKS_NT_OUT  // streaming (non-temporal) output stores (smooth_impl.hpp)
+        __builtin_nontemporal_store(cm[0], outb + t * a.ot);
+        __builtin_nontemporal_store(cm[1], outb + t * a.ot + 1);
+#else
         *(double2 *)(outb + t * a.ot) = make_double2(cm[0], cm[1]);
+#endif
       } else {
         project_store<R, N, CI>(outb + t * a.ot, a.oj, md.C, ms, md.off);
       }
