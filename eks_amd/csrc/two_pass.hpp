@@ -172,8 +172,13 @@ struct YevRing {
   EKS_DEV void fetch(int slot, long long t) {
 #pragma unroll
     for (int j = 0; j < N; ++j) {
+#if EKS_NT_LOAD
+      y[slot][j] = __builtin_nontemporal_load(&pl(yb, t * N + j, B, b));
+      ev[slot][j] = __builtin_nontemporal_load(&pl(eb, t * N + j, B, b));
+#else
       y[slot][j] = pl(yb, t * N + j, B, b);
       ev[slot][j] = pl(eb, t * N + j, B, b);
+#endif
     }
   }
   EKS_DEV void get(int slot, double (&avg)[N], double (&rv)[N]) const {
