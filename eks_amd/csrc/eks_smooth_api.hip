@@ -12,17 +12,18 @@ namespace {
 // trajectory (B alone fills the GPU); the two-pass algorithm 3 for the
 // (r, n) = (2, 2) single-view shape with many trajectories (whole 256-lane
 // blocks per chunk) and compile-time member counts; else the three-pass
-// time-parallel scan.  A requested time-parallel run with a single chunk
-// runs sequentially.
+// time-parallel scan.  A requested algo 2 with a single chunk runs
+// sequentially; a requested algo 3 runs at any T (compiled E).
 int pick_algo(long long B, long long T, int n, int r, int E, int algo) {
   const long long L = chunk_len(B, T, r);
   if (algo == 1) return 1;
+  const bool a3_ok = E >= 3 && E <= 5;  // compiled member counts; any T
+  if (algo == 3 && a3_ok) return 3;
   if (L >= T) return 1;
-  const bool a3_ok = (E >= 3 && E <= 5) && T >= 2 * fine_len3(r, n);
-  if (algo == 3) return a3_ok ? 3 : 2;
+  if (algo == 3) return 2;
   if (algo == 2) return 2;
   const bool many = uniform_lanes(B) && B >= 2048;
-  return (a3_ok && many && r == 2 && n == 2) ? 3 : 2;
+  return (a3_ok && many && r == 2 && n == 2 && T >= 2 * fine_len3(r, n)) ? 3 : 2;
 }
 
 bool shape_compiled(int r, int n) {

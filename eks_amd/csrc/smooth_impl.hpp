@@ -1635,7 +1635,7 @@ int dispatch_members_c(int E, F &&f) {
 
 template <int R, int N, int AI, int CI>
 int launch_shape(const SmoothArgs &a, int algo, long long L) {
-  if (algo == 3) return launch_algo3_split<R, N, AI, CI>(a);
+  if (algo == 3) return launch_algo3<R, N, AI, CI>(a);
   const bool f32 = a.dtype == EKS_F32;
   const bool yev = a.dtype == EKS_YEV32 || a.dtype == EKS_YEV64;
   if (algo == 1) {

@@ -731,10 +731,11 @@ def test_fit_yev_handoff_bit_exact(torch, kind, V, E, dtype, mode, algo):
 
 
 def test_algo3_batch_slices_bit_identical(torch):
-    """algo 3's chunking (16-frame fine chunks, 64-frame coarse chunks, 8 * S
-    scan parts) depends on T and the coarse scan's sub-part count S only:
-    smoothing a slice of the trajectories with the same S (here 4 for every
-    B <= 3072) gives bit-identical results to smoothing all of them."""
+    """algo 3's chained passes combine a unit's aggregate only with its
+    neighbour's published value, so every operation's association order
+    depends on T alone: smoothing a slice of the trajectories (ragged last
+    64-trajectory group included) gives bit-identical results to smoothing
+    all of them, and so does a second call (no timing dependence)."""
     from eks_amd import _lib, batch, synthetic
     rng = np.random.default_rng(21)
     B, T, E = 1100, 600, 5
@@ -744,6 +745,9 @@ def test_algo3_batch_slices_bit_identical(torch):
     flags = _lib.EKS_MODEL_A_IDENTITY | _lib.EKS_MODEL_C_IDENTITY
     full = batch.smooth(d, params, n=2, r=2, algo=3, flags=flags, want_ms=True, want_nll=True)
     assert (full["status"] == 0).all()
+    again = batch.smooth(d, params, n=2, r=2, algo=3, flags=flags, want_ms=True, want_nll=True)
+    assert torch.equal(again["out"], full["out"])
+    assert torch.equal(again["nll"], full["nll"])
     for lo, hi in ((0, 70), (600, 700), (1030, 1100)):           # first half, boundary, second half
         part = batch.smooth(d[lo:hi], params[lo:hi].contiguous(), n=2, r=2, algo=3, flags=flags,
                             want_ms=True, want_nll=True)
@@ -752,24 +756,26 @@ def test_algo3_batch_slices_bit_identical(torch):
         assert torch.equal(part["nll"], full["nll"][lo:hi]), (lo, hi)
 
 
-@pytest.mark.parametrize("S", [1, 2, 4, 8])
-def test_algo3_coarse_subparts(torch, S, monkeypatch):
-    """The coarse scan's sub-part count S (picked from B; EKS_K3_S pins it)
-    changes the partition of the coarse chunks into scan parts: every S must
-    reproduce the sequential recursion, including parts that are empty
-    (T short enough that some of the 8 * S parts hold no coarse chunk)."""
+@pytest.mark.parametrize("B", [1, 63, 300, 2100])
+def test_algo3_chain_lengths(torch, B):
+    """The chained passes over every chain length: T from one partial fine
+    chunk (17 frames) to hundreds of coarse chunks, partial last fine and
+    coarse chunks (T not a multiple of 16 / 64), one or many 64-trajectory
+    groups with a ragged last one.  Against the sequential recursion (algo 1):
+    outputs and smoothed means < 1e-8, NLL rtol 1e-10, no status bits."""
     from eks_amd import _lib, batch, synthetic
-    rng = np.random.default_rng(40 + S)
-    B, E = 300, 5
+    rng = np.random.default_rng(40 + B)
+    E = 5
     flags = _lib.EKS_MODEL_A_IDENTITY | _lib.EKS_MODEL_C_IDENTITY
-    for T in (2000, 700, 64, 17):       # 32, 11, 1 and 1 coarse chunks
+    for T in (17, 64, 65, 700, 4003):
+        if B * T > 2100 * 700:
+            continue
         st = synthetic.singleview_obs(rng, E, T, K=B).transpose(2, 0, 1, 3).astype(np.float32)
         d = batch.make_time_major(st, dtype=np.float32)
         params = batch.fit(d, kind="singleview", n=2, r=2, smooth_param=0.01, quantile_keep=25)[0]
         ref = batch.smooth(d, params, n=2, r=2, algo=1, flags=flags, want_ms=True, want_nll=True)
-        monkeypatch.setenv("EKS_K3_S", str(S))
         got = batch.smooth(d, params, n=2, r=2, algo=3, flags=flags, want_ms=True, want_nll=True)
-        monkeypatch.delenv("EKS_K3_S")
+        assert _lib.load().eks_smooth_algo(B, T, 2, 2, E, 3) == 3, T
         assert (got["status"] == 0).all(), T
         assert float((got["out"] - ref["out"]).abs().max()) < 1e-8, T
         assert float((got["ms"] - ref["ms"]).abs().max()) < 1e-8, T
@@ -811,34 +817,3 @@ def test_filter_only_closed_form_nll(torch, kind, B, T):
     o2 = batch.smooth(one, p1, n=n, r=r, algo=2, flags=flags)["out"]
     o1 = batch.smooth(one, p1, n=n, r=r, algo=1, flags=flags)["out"]
     assert float((o2 - o1).abs().max()) < 1e-8
-
-
-@pytest.mark.parametrize("mode", [1, 2])
-def test_algo3_split_streams(torch, mode, monkeypatch):
-    """EKS_A3_SPLIT = 1 / 2 runs algo 3 from 8 192 trajectories as two
-    half-batches on two streams (two_pass.hpp launch_algo3_split; half A =
-    whole 64-trajectory groups).  The split call must equal two separate
-    calls on the halves bit for bit (each below the split threshold, so one
-    stream each), and the sequential recursion (algo 1) to < 1e-8 px / NLL
-    rtol 1e-10, ragged last group included."""
-    from eks_amd import _lib, batch, synthetic
-    monkeypatch.setenv("EKS_A3_SPLIT", str(mode))
-    rng = np.random.default_rng(22)
-    B, T, E = 8200, 300, 5
-    b0 = (B // 2 + 63) // 64 * 64
-    st = synthetic.singleview_obs(rng, E, T, K=B).transpose(2, 0, 1, 3).astype(np.float32)
-    d = batch.make_time_major(st, dtype=np.float32)               # (B, T, E, 2) view
-    params = batch.fit(d, kind="singleview", n=2, r=2, smooth_param=0.01, quantile_keep=25)[0]
-    flags = _lib.EKS_MODEL_A_IDENTITY | _lib.EKS_MODEL_C_IDENTITY
-    full = batch.smooth(d, params, n=2, r=2, algo=3, flags=flags, want_ms=True, want_nll=True)
-    assert (full["status"] == 0).all()
-    for lo, hi in ((0, b0), (b0, B)):
-        part = batch.smooth(d[lo:hi], params[lo:hi].contiguous(), n=2, r=2, algo=3, flags=flags,
-                            want_ms=True, want_nll=True)
-        assert torch.equal(part["out"], full["out"][lo:hi]), (lo, hi)
-        assert torch.equal(part["ms"], full["ms"][lo:hi]), (lo, hi)
-        assert torch.equal(part["nll"], full["nll"][lo:hi]), (lo, hi)
-        assert torch.equal(part["status"], full["status"][lo:hi]), (lo, hi)
-    ref = batch.smooth(d, params, n=2, r=2, algo=1, flags=flags, want_nll=True)
-    assert float((full["out"] - ref["out"]).abs().max()) < 1e-8
-    np.testing.assert_allclose(full["nll"].cpu().numpy(), ref["nll"].cpu().numpy(), rtol=1e-10)
