@@ -301,8 +301,10 @@ def workload_singleview(torch, a, dev, rank, world, config):
                          trajectories_per_rank=B, smooth_param=a.smooth_param,
                          quantile_keep=a.quantile_keep),
                 shape=(B, T, 2, 2, E),
-                key=f"config{config}-singleview-v{len(videos) * world if config == 4 else 1}"
-                    f"-k{K}-e{E}-t{T}-n{world}-{a.scaling}",
+                # PMC traffic is a property of one rank's launch: keyed by the
+                # rank's own shard (videos per rank), so an N-rank line finds
+                # the profile of an N = 1 run of the same shard size
+                key=f"config{config}-singleview-v{len(videos)}-k{K}-e{E}-t{T}",
                 out=out, videos=videos)
 
 
@@ -351,13 +353,13 @@ def workload_multiview(torch, a, dev, rank, world):
                 units=K * T, bytes_per_unit=E * n * 4 + n * 8, cpu_plan=cpu_plan, desc=desc,
                 cfg=dict(cameras=V, keypoints=K, members=E, frames=T,
                          smooth_param=a.smooth_param, quantile_keep=a.quantile_keep),
-                shape=(K, T, n, 3, E), key=f"config3-multiview-k{K}-e{E}-t{T}-n{world}")
+                shape=(K, T, n, 3, E), key=f"config3-multiview-k{K}-e{E}-t{T}")
 
 
 def workload_pupil(torch, a, dev, rank, world):
     """config 5: IBL pupil, 1M frames x 4 keypoints, NLL sweep + smooth."""
     import numpy as np
-    from eks_amd import batch, fit, synthetic
+    from eks_amd import _lib, batch, fit, synthetic
     E, T = a.members, a.frames
     st = synthetic.pupil_obs(np.random.default_rng(a.seed), E, T, a=0.99)  # (E, T, 8) f32
     obs_tm = torch.from_numpy(np.ascontiguousarray(st.transpose(1, 0, 2))).to(dev)  # (T, E, 8)
@@ -379,6 +381,7 @@ def workload_pupil(torch, a, dev, rank, world):
     out = torch.empty((T, 1, 8), dtype=torch.float64, device=dev).permute(1, 0, 2)
     ms = torch.empty((1, T, 3), dtype=torch.float64, device=dev)
     status = torch.empty((1,), dtype=torch.int32, device=dev)
+    sweep_status = torch.empty((len(cands),), dtype=torch.int32, device=dev)
     cands_obs = obs.expand(len(cands), -1, -1, -1)  # batch stride 0: members shared
     # pupil structure (C = pupil matrix, A / Q diagonal): EKS_MODEL_PUPIL kernels
     flags = 0 if a.dense_pupil else batch.model_flags(stackp("A"), stackp("C"), stackp("Q"))
@@ -401,7 +404,8 @@ def workload_pupil(torch, a, dev, rank, world):
         status.copy_(r["status"])
 
     def step():
-        scores = batch.nll(cands_obs, params, n=8, r=3, algo=a.algo, check=False, flags=flags)
+        scores = batch.nll(cands_obs, params, n=8, r=3, algo=a.algo, check=False, flags=flags,
+                           status=sweep_status)
         best = torch.argmin(scores)                                    # stays on device
         p_best = params.index_select(0, best.view(1)).contiguous()
         r = batch.smooth(obs, p_best, n=8, r=3, out=out, want_ms=True, status=status,
@@ -421,9 +425,17 @@ def workload_pupil(torch, a, dev, rank, world):
         pm = fit.pupil_model(O.ensemble_array(pre)[0], cands[b]["A"])
         pb = batch.pack_params(pm["m0"], pm["S0"], pm["A"], pm["Q"], pm["C"], pm["offset"],
                                device=dev)
-        g = batch.smooth(obs[:, :Tc], pb, n=8, r=3)["out"][0].cpu().numpy()
+        # the timed step's kernels (same model flags: the EKS_MODEL_PUPIL
+        # kernels unless --dense-pupil) on the same prefix
+        fb = 0 if a.dense_pupil else batch.model_flags(pm["A"][None], pm["C"][None], pm["Q"][None])
+        g = batch.smooth(obs[:, :Tc], pb, n=8, r=3, flags=fb, check=True)["out"][0].cpu().numpy()
+        # the sweep's scores on the same prefix, for the candidates the 1-core
+        # run scores (tasks 0 and 1): relative NLL difference
+        nll_gpu = batch.nll(cands_obs[:2, :Tc], params[:2].contiguous(), n=8, r=3, flags=flags,
+                            check=True).cpu().numpy()
         half = len(cands) // 2
         return dict(tasks=tasks, gpu={len(cands): g}, units_all=4 * Tc, units_one=4 * Tc,
+                    nll_gpu={0: float(nll_gpu[0]), 1: float(nll_gpu[1])},
                     one=[0, 1, len(cands)], weights=[half, half, 1],
                     what=f"first {Tc} frames x 4 keypoints: NLL of {{n}} of the {len(cands)} "
                          f"candidate models + smoothing the chosen one")
@@ -433,7 +445,17 @@ def workload_pupil(torch, a, dev, rank, world):
             f"batched) + smoothing of the argmin, float64")
     if a.timeshard:
         desc += f"; frames split over {world} rank(s) (time-sharded scan)"
+    def post_check():
+        # after the timed loop: no scan breakdown / singular system in the
+        # sweep (its NLLs feed the argmin unchecked) or in the final smooth
+        bad = _lib.EKS_STATUS_SCAN | _lib.EKS_STATUS_SINGULAR
+        if not a.timeshard and int((sweep_status & bad).sum().item()) != 0:
+            raise RuntimeError("config 5: the NLL sweep reported a scan breakdown / singular system")
+        if int((status & bad).sum().item()) != 0:
+            raise RuntimeError("config 5: the final smooth reported a scan breakdown / singular system")
+
     return dict(step=step_timeshard if a.timeshard else step, status=status, units=4 * Tk,
+                post_check=post_check,
                 bytes_per_unit=(32 * E + 88) / 4, cpu_plan=cpu_plan, desc=desc,
                 timeshard=a.timeshard,
                 # k_c1_elem: one element-absorb step per (candidate, frame); flops counted
@@ -445,22 +467,24 @@ def workload_pupil(torch, a, dev, rank, world):
                            unit_is="element-absorb step"),
                 cfg=dict(frames=T, keypoints=4, members=E, candidates=len(cands)),
                 shape=(1, T, 8, 3, E),
-                key=f"config5-pupil-t{T}-n{world}{'-ts' if a.timeshard else ''}",
+                key=f"config5-pupil-t{T}" + (f"-ts-n{world}" if a.timeshard else ""),
                 extra=lambda: dict(
                     sweep_candidates=len(cands),
                     best_model=[float(x) for x in np.diag(cands[int(state['best'])]['A'])]))
 
 
-def load_pmc(workload_key):
-    # PMC summary of the same workload (tools/gpu_profile.sh -> tools/prof_summary.py)
-    path = os.path.join(HERE, "bench_pmc.json")
+def load_pmc(workload_key, path=None):
+    """PMC summary of one rank's launch of this workload (tools/gpu_profile.sh
+    -> tools/prof_summary.py): bench_pmc.json holds one entry per workload
+    key (per-rank shard), or None."""
+    path = path or os.path.join(HERE, "bench_pmc.json")
     if not os.path.exists(path):
         return None
     try:
         d = json.load(open(path))
     except Exception:
         return None
-    return d if d.get("workload_key") == workload_key else None
+    return (d.get("entries") or {}).get(workload_key)
 
 
 def launch_ranks(a) -> int:
@@ -477,6 +501,80 @@ def launch_ranks(a) -> int:
            "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
     return subprocess.call(cmd, env=env)
+
+
+def runs_cpu_baseline(rank, a) -> bool:
+    """The CPU baseline runs on rank 0's own shard after the timed loop, at
+    any N (for N > 1 the other ranks wait at the final barrier)."""
+    return rank == 0 and not a.no_cpu_baseline
+
+
+def make_line(a, w, world, algo_used, units_local, units_total, elapsed_max, kernels,
+              kern_ms_max, cpu, maxdiff, e2e, cpu_e2e, gather_ms, gather_bytes, setup_s,
+              hip_graph, backend, pmc_path=None):
+    """The one JSON line rank 0 prints (the driver's bench contract).  At N > 1
+    the roofline, traffic and CPU baseline describe rank 0's own launch (its
+    shard); ``value`` is the whole job's units over the max-over-ranks time."""
+    value = units_total / elapsed_max * a.steps
+    achieved = w["bytes_per_unit"] * units_local / (kern_ms_max * 1e-3) / 1e9
+    pmc = load_pmc(w["key"], pmc_path)
+    scaling = ("strong" if (a.config == 4 and a.scaling == "strong") or w.get("timeshard")
+               else "weak")
+    par = (f"videos sharded over {world} rank(s), no data-path collective" if a.config == 4
+           else f"frames split over {world} rank(s), 2 all_gathers of segment aggregates"
+           if w.get("timeshard") else f"{world} independent replica(s)")
+    line = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "kp-ts/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": elapsed_max / a.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": scaling,
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic",
+        "config": dict(workload=w["desc"], algo=algo_used, parallelism=par, **w["cfg"]),
+        "roofline": {
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": PEAK_HBM_GBS,
+            "unit": "GB/s",
+            "frac": achieved / PEAK_HBM_GBS,
+            "traffic": (pmc or {}).get("hbm_bytes_per_launch"),
+            "traffic_key": w["key"],
+            "kernel": "eks_smooth (" + " + ".join(n for n, _ in kernels) + ")",
+            "kernel_ms": kern_ms_max,
+            "kernels_ms": {n: round(ms, 4) for n, ms in kernels},
+            "bytes_per_unit": w["bytes_per_unit"],
+            "units_per_launch": units_local,
+        },
+        "cpu_baseline": cpu,
+        "max_abs_diff_vs_cpu": maxdiff,
+        "end_to_end": None if e2e is None else dict(e2e, cpu_value=cpu_e2e),
+        "setup_s": round(setup_s, 2),
+        "hip_graph": hip_graph,
+    }
+    if "flops" in w:  # an FP64-issue-bound kernel: its flop roofline beside the HBM one
+        f = w["flops"]
+        kms = dict(kernels).get(f["kernel"])
+        if kms:
+            tf = f["per_unit"] * f["units"] / (kms * 1e-3) / 1e12
+            line["flop_roofline"] = dict(kernel=f["kernel"], bound="fp64 valu", achieved=tf,
+                                         peak=PEAK_FP64_TFS, unit="TFLOP/s",
+                                         frac=tf / PEAK_FP64_TFS, flops_per_unit=f["per_unit"],
+                                         units_per_launch=f["units"], unit_is=f["unit_is"])
+    if "extra" in w:
+        line.update(w["extra"]())
+    if world > 1:
+        line["distributed"] = dict(world_size=world, backend=backend, units_per_rank=units_local,
+                                   roofline_scope="rank 0's launch (per-rank shard)")
+    if gather_ms is not None:
+        line["gather_ms"] = gather_ms
+        line["gather_bytes"] = gather_bytes
+    return line
 
 
 def main():
@@ -541,6 +639,8 @@ def main():
     dist.barrier()
     elapsed = time.perf_counter() - t0
     elapsed_max = dist.max_over_ranks(elapsed, device=dev)
+    if "post_check" in w:
+        w["post_check"]()
     # per-kernel launch durations: HIP events recorded by libeks_hip on the
     # launch stream around each kernel of each eks_smooth call (separate pass,
     # so the events do not perturb the timed loop above)
@@ -604,8 +704,9 @@ def main():
 
     cpu = None
     maxdiff = None
+    nll_rel = None
     cpu_e2e = None
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+    if runs_cpu_baseline(rank, a):
         cores = cpu_cores() if a.cpu_cores is None else a.cpu_cores
         plan = w["cpu_plan"](cores)
         tasks = plan["tasks"]
@@ -619,6 +720,8 @@ def main():
         diffs += [float(abs(outs1[j] - plan["gpu"][i]).max())
                   for j, i in enumerate(plan["one"]) if i in plan["gpu"]]
         maxdiff = max(diffs)
+        if plan.get("nll_gpu"):  # candidate NLLs: GPU sweep vs the oracle's compute_nll
+            nll_rel = max(abs(outs1[j] - v) / abs(outs1[j]) for j, v in plan["nll_gpu"].items())
         if plan.get("weights") is None:
             cpu_e2e = plan["units_one"] / (t_fit1 + t_hot1)
         if plan.get("weights") is not None:
@@ -635,65 +738,15 @@ def main():
                    host_cpus=len(os.sched_getaffinity(0)))
 
     if rank == 0:
-        value = units_total / elapsed_max * a.steps
-        achieved = w["bytes_per_unit"] * units_local / (kern_ms_max * 1e-3) / 1e9
-        pmc = load_pmc(w["key"])
-        scaling = ("strong" if (a.config == 4 and a.scaling == "strong") or w.get("timeshard")
-                   else "weak")
-        par = (f"videos sharded over {world} rank(s), no data-path collective" if a.config == 4
-               else f"frames split over {world} rank(s), 2 all_gathers of segment aggregates"
-               if w.get("timeshard") else f"{world} independent replica(s)")
-        line = {
-            "metric": METRIC,
-            "value": value,
-            "unit": "kp-ts/s",
-            "n_gpus": world,
-            "steps": a.steps,
-            "warmup": a.warmup,
-            "ms_per_step": elapsed_max / a.steps * 1e3,
-            "higher_is_better": True,
-            "scaling": scaling,
-            "vs_baseline": None,
-            "dtype": "f64",
-            "data": "synthetic",
-            "config": dict(workload=w["desc"], algo=algo_used, parallelism=par, **w["cfg"]),
-            "roofline": {
-                "bound": "hbm",
-                "achieved": achieved,
-                "peak": PEAK_HBM_GBS,
-                "unit": "GB/s",
-                "frac": achieved / PEAK_HBM_GBS,
-                "traffic": (pmc or {}).get("hbm_bytes_per_launch"),
-                "kernel": "eks_smooth (" + " + ".join(n for n, _ in kernels) + ")",
-                "kernel_ms": kern_ms_max,
-                "kernels_ms": {n: round(ms, 4) for n, ms in kernels},
-                "bytes_per_unit": w["bytes_per_unit"],
-                "units_per_launch": units_local,
-            },
-            "cpu_baseline": cpu,
-            "max_abs_diff_vs_cpu": maxdiff,
-            "end_to_end": None if e2e is None else dict(e2e, cpu_value=cpu_e2e),
-            "setup_s": round(setup_s, 2),
-            "hip_graph": graph is not None,
-        }
-        if "flops" in w:  # an FP64-issue-bound kernel: its flop roofline beside the HBM one
-            f = w["flops"]
-            kms = dict(kernels).get(f["kernel"])
-            if kms:
-                tf = f["per_unit"] * f["units"] / (kms * 1e-3) / 1e12
-                line["flop_roofline"] = dict(kernel=f["kernel"], bound="fp64 valu", achieved=tf,
-                                             peak=PEAK_FP64_TFS, unit="TFLOP/s",
-                                             frac=tf / PEAK_FP64_TFS, flops_per_unit=f["per_unit"],
-                                             units_per_launch=f["units"], unit_is=f["unit_is"])
-        if "extra" in w:
-            line.update(w["extra"]())
+        backend = None
         if world > 1:
             import torch.distributed as tdist
-            line["distributed"] = dict(world_size=tdist.get_world_size(),
-                                       backend=str(tdist.get_backend()))
-        if gather_ms is not None:
-            line["gather_ms"] = gather_ms
-            line["gather_bytes"] = gather_bytes
+            backend = str(tdist.get_backend())
+        line = make_line(a, w, world, algo_used, units_local, units_total, elapsed_max, kernels,
+                         kern_ms_max, cpu, maxdiff, e2e, cpu_e2e, gather_ms, gather_bytes,
+                         setup_s, graph is not None, backend)
+        if nll_rel is not None:
+            line["nll_rel_diff_vs_cpu"] = nll_rel
         print(json.dumps(line))
     dist.barrier()
 

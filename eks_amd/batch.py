@@ -231,14 +231,15 @@ def fit(obs, *, kind: str, n: int, r: int, smooth_param: float, quantile_keep: f
 
 
 def nll(obs, params, *, n: int, r: int, mode: str = "median", flags: int = 0, algo: int = 0,
-        check: bool = True):
+        check: bool = True, status=None):
     """Filter-only pass: the innovation NLL of every
     trajectory / candidate model, no backward pass.  To score C candidate
     models of ONE trajectory, pass ``obs.expand(C, -1, -1, -1)`` (batch
     stride 0: the members are read once per candidate from the same memory)
-    and C rows of params."""
+    and C rows of params.  ``status`` (B,) int32 receives the per-trajectory
+    status bits (check=False callers read it themselves)."""
     return smooth(obs, params, n=n, r=r, mode=mode, flags=flags, algo=algo, check=check,
-                  want_out=False)["nll"]
+                  want_out=False, status=status)["nll"]
 
 
 def status_bits(status) -> int:

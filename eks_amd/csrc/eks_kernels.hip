@@ -367,6 +367,279 @@ __global__ void k_kalman_dot(int k, const double *x, const double *Vg, const dou
   if (status) status[0] = ok ? 0 : EKS_STATUS_SINGULAR;
 }
 
+// ------------------------------------------------------------------------
+// A2/A3 for any n <= kMaxObsRt (5+ cameras): one wave per trajectory, the
+// n x n system of kalman_dot in LDS with lane i owning row i, solved by the
+// elimination of gauss_solve (partial pivoting, first maximum); every sum in
+// the order of k_forward_dense, so n <= 8 inputs give the compiled kernel's
+// numbers.  Latency bound (O(n) dependent elimination rounds per step): the
+// reference's own per-step solve, for the drop-in API -- eks_smooth's fused
+// kernels are the throughput path.
+// ------------------------------------------------------------------------
+struct RtLds {  // LDS layout of the runtime-n solve (doubles)
+  int n, nc, ld;
+  size_t a, rhs, pct, e0, cs, ctx, total;
+  __host__ __device__ RtLds(int n_, int r) : n(n_), nc(1 + r), ld(n_ + 1) {
+    a = 0;
+    rhs = a + (size_t)n * ld;
+    pct = rhs + (size_t)n * nc;
+    e0 = pct + (size_t)r * n;
+    cs = e0 + n;
+    ctx = cs + (size_t)n * r;
+    total = ctx + (size_t)r * nc;
+  }
+};
+
+// Solve a X = rhs in LDS (a: n x n, stride ld; rhs: n x nc), one wave.
+// Returns the pivots' |det| accumulation like gauss_solve; ok false on a
+// zero pivot.  Lane i < n owns row i.
+EKS_DEV bool lds_gauss_solve(double *a, double *rhs, int n, int ld, int nc, double &det_m,
+                             int &det_e) {
+  const int l = threadIdx.x;
+  bool ok = true;
+  for (int k = 0; k < n; ++k) {
+    // the first maximum of |a[i][k]|, i >= k (NaNs never win, as in the
+    // compiled bubble: a NaN pivot candidate keeps its row)
+    const double akk = a[k * ld + k];
+    int p = k;
+    if (akk == akk) {
+      double v = (l > k && l < n) ? fabs(a[l * ld + k]) : -1.0;
+      if (!(v == v)) v = -1.0;
+      int idx = l;
+      double best = fabs(akk);
+      // lanes with v > |a[k][k]| compete; ties -> smallest index
+      double cv = v > best ? v : -1.0;
+      int ci = v > best ? idx : n;
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) {
+        const double ov = __shfl_xor(cv, off, 64);
+        const int oi = __shfl_xor(ci, off, 64);
+        if (ov > cv || (ov == cv && oi < ci)) {
+          cv = ov;
+          ci = oi;
+        }
+      }
+      if (ci < n) p = ci;
+    }
+    if (p != k) {
+      for (int j = l; j < n; j += 64)
+        if (j >= k) {
+          const double t = a[k * ld + j];
+          a[k * ld + j] = a[p * ld + j];
+          a[p * ld + j] = t;
+        }
+      if (l < nc) {
+        const double t = rhs[k * nc + l];
+        rhs[k * nc + l] = rhs[p * nc + l];
+        rhs[p * nc + l] = t;
+      }
+    }
+    __syncthreads();
+    const double piv = a[k * ld + k];
+    ok = ok && (piv != 0.0);
+    int e;
+    det_m = frexp(det_m * fabs(piv), &e);
+    det_e += e;
+    const double inv = 1.0 / piv;
+    if (l > k && l < n) {
+      const double f = a[l * ld + k] * inv;
+      for (int j = k + 1; j < n; ++j) a[l * ld + j] = fma(-f, a[k * ld + j], a[l * ld + j]);
+      for (int c = 0; c < nc; ++c) rhs[l * nc + c] = fma(-f, rhs[k * nc + c], rhs[l * nc + c]);
+    }
+    __syncthreads();
+  }
+  if (l < nc) {  // back substitution, one rhs column per lane
+    for (int k = n - 1; k >= 0; --k) {
+      double sum = rhs[k * nc + l];
+      for (int i = k + 1; i < n; ++i) sum = fma(-a[k * ld + i], rhs[i * nc + l], sum);
+      rhs[k * nc + l] = sum / a[k * ld + k];
+    }
+  }
+  __syncthreads();
+  return ok;
+}
+
+template <int R>
+__global__ __launch_bounds__(64) void k_forward_dense_rt(
+    long long B, long long TT, int n, const double *__restrict__ y, const double *__restrict__ ev,
+    const double *__restrict__ m0g, const double *__restrict__ S0g, const double *__restrict__ Ag,
+    const double *__restrict__ Qg, const double *__restrict__ Cg, const double *__restrict__ Rg,
+    int shared, double *__restrict__ mf, double *__restrict__ Vf, double *__restrict__ S,
+    double *__restrict__ nll, int32_t *__restrict__ status) {
+  extern __shared__ double sh[];
+  const long long b = blockIdx.x;
+  const int l = threadIdx.x;
+  if (b >= B) return;
+  const RtLds L(n, R);
+  double *a = sh + L.a, *rhs = sh + L.rhs, *pct = sh + L.pct, *e0s = sh + L.e0, *Cs = sh + L.cs,
+         *ctx = sh + L.ctx;
+  const int nc = L.nc, ld = L.ld;
+  const long long pb = shared ? 0 : b;
+  double A[R][R], Q[R][R], m[R], P[R][R];
+  load_mat<R, R>(Ag + pb * R * R, A);
+  load_mat<R, R>(Qg + pb * R * R, Q);
+  load_vec<R>(m0g + pb * R, m);
+  load_mat<R, R>(S0g + pb * R * R, P);
+  const double *Cb = Cg + pb * (long long)n * R;
+  const double *Rb = Rg ? Rg + pb * (long long)n * n : nullptr;
+  for (int i = l; i < n * R; i += 64) Cs[i] = Cb[i];
+  __syncthreads();
+  const double *yb = y + b * TT * n;
+  const double *eb = ev + b * TT * n;
+  double *mfb = mf ? mf + b * TT * R : nullptr;
+  double *Vfb = Vf ? Vf + b * TT * R * R : nullptr;
+  double *Sb = S ? S + b * TT * R * R : nullptr;
+  bool ok = true;
+  double quad = 0.0, det_m = 1.0;
+  int det_e = 0;
+  double mprev[R], Vprev[R][R];
+  for (long long t = 0; t < TT; ++t) {
+    if (t > 0) {
+      double VAt[R][R];
+      matmul_nt<R, R, R>(Vprev, A, VAt);
+      matmul<R, R, R>(A, VAt, P);
+#pragma unroll
+      for (int i = 0; i < R; ++i)
+#pragma unroll
+        for (int j = 0; j < R; ++j) P[i][j] += Q[i][j];
+      matvec<R, R>(A, mprev, m);
+      if (Sb && l == 0) store_mat<R, R>(Sb + (t - 1) * R * R, P);
+    } else if (Sb && l == 0) {
+      store_mat<R, R>(Sb, P);
+    }
+    // P C^T (R x n): lane j computes column j
+    if (l < n) {
+#pragma unroll
+      for (int k = 0; k < R; ++k) {
+        double sum = 0.0;
+#pragma unroll
+        for (int q = 0; q < R; ++q) sum = fma(P[k][q], Cs[l * R + q], sum);
+        pct[k * n + l] = sum;
+      }
+    }
+    __syncthreads();
+    if (l < n) {  // row l of R_t + C (P C^T) and of [ y - C m | C P ]
+      double Cl[R];
+#pragma unroll
+      for (int k = 0; k < R; ++k) Cl[k] = Cs[l * R + k];
+      for (int j = 0; j < n; ++j) {
+        double sum = 0.0;
+#pragma unroll
+        for (int k = 0; k < R; ++k) sum = fma(Cl[k], pct[k * n + j], sum);
+        sum += (l == j) ? eb[t * n + l] : (Rb ? Rb[(long long)l * n + j] : 0.0);
+        a[l * ld + j] = sum;
+      }
+      double cm = 0.0;
+#pragma unroll
+      for (int k = 0; k < R; ++k) cm = fma(Cl[k], m[k], cm);
+      const double e = yb[t * n + l] - cm;
+      e0s[l] = e;
+      rhs[l * nc] = e;
+#pragma unroll
+      for (int j = 0; j < R; ++j) {
+        double sum = 0.0;
+#pragma unroll
+        for (int k = 0; k < R; ++k) sum = fma(Cl[k], P[k][j], sum);
+        rhs[l * nc + 1 + j] = sum;
+      }
+    }
+    __syncthreads();
+    ok = lds_gauss_solve(a, rhs, n, ld, nc, det_m, det_e) && ok;
+    // quad += e0 . x0 (in row order); C^T [x0 | X] (R x nc), one lane per entry
+    if (l == 0)
+      for (int i = 0; i < n; ++i) quad = fma(e0s[i], rhs[i * nc], quad);
+    if (l < R * nc) {
+      const int k = l / nc, c = l % nc;
+      double sum = 0.0;
+      for (int i = 0; i < n; ++i) sum = fma(Cs[i * R + k], rhs[i * nc + c], sum);
+      ctx[k * nc + c] = sum;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      double sum = 0.0;
+#pragma unroll
+      for (int k = 0; k < R; ++k) sum = fma(P[i][k], ctx[k * nc], sum);
+      mprev[i] = m[i] + sum;
+#pragma unroll
+      for (int j = 0; j < R; ++j) {
+        double u = 0.0;
+#pragma unroll
+        for (int k = 0; k < R; ++k) u = fma(P[i][k], ctx[k * nc + 1 + j], u);
+        Vprev[i][j] = P[i][j] - u;
+      }
+    }
+    if (l == 0) {
+      if (mfb) store_vec<R>(mfb + t * R, mprev);
+      if (Vfb) store_mat<R, R>(Vfb + t * R * R, Vprev);
+    }
+    __syncthreads();  // LDS reused by the next step
+  }
+  if (l == 0) {
+    if (Sb && TT >= 2) {
+      double z[R][R] = {};
+      store_mat<R, R>(Sb + (TT - 1) * R * R, z);
+    }
+    if (nll) nll[b] = 0.5 * ((double)TT * n * kLog2Pi + log(det_m) + det_e * kLn2 + quad);
+    if (status) status[b] = ok ? 0 : EKS_STATUS_SINGULAR;
+  }
+}
+
+// kalman_dot for any n <= kMaxObsRt: one wave, the same LDS solve
+template <int R>
+__global__ __launch_bounds__(64) void k_kalman_dot_rt(int n, int k, const double *x, const double *Vg,
+                                                      const double *Cg, const double *Rg,
+                                                      double *out, int32_t *status) {
+  extern __shared__ double sh[];
+  const int l = threadIdx.x;
+  const RtLds L(n, 0);  // rhs: one column at a time (nc = 1)
+  double *a = sh + L.a, *rhs = sh + L.rhs;
+  double *vct = sh + L.total;  // V C^T (R x n)
+  double V[R][R];
+  load_mat<R, R>(Vg, V);
+  if (l < n) {
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      double sum = 0.0;
+#pragma unroll
+      for (int q = 0; q < R; ++q) sum = fma(V[i][q], Cg[l * R + q], sum);
+      vct[i * n + l] = sum;
+    }
+  }
+  __syncthreads();
+  bool ok = true;
+  for (int c = 0; c < k; ++c) {
+    if (l < n) {
+      for (int j = 0; j < n; ++j) {
+        double sum = 0.0;
+#pragma unroll
+        for (int q = 0; q < R; ++q) sum = fma(Cg[l * R + q], vct[q * n + j], sum);
+        a[l * L.ld + j] = sum + Rg[(long long)l * n + j];
+      }
+      rhs[l] = x[l * k + c];
+    }
+    __syncthreads();
+    double dm = 1.0;
+    int de = 0;
+    ok = lds_gauss_solve(a, rhs, n, L.ld, 1, dm, de) && ok;
+    if (l < R) {
+      double ct[R];
+#pragma unroll
+      for (int q = 0; q < R; ++q) {
+        double sum = 0.0;
+        for (int i = 0; i < n; ++i) sum = fma(Cg[i * R + q], rhs[i], sum);
+        ct[q] = sum;
+      }
+      double sum = 0.0;
+#pragma unroll
+      for (int q = 0; q < R; ++q) sum = fma(V[l][q], ct[q], sum);
+      out[l * k + c] = sum;
+    }
+    __syncthreads();
+  }
+  if (l == 0 && status) status[0] = ok ? 0 : EKS_STATUS_SINGULAR;
+}
+
 }  // namespace eks
 
 // ==========================================================================
@@ -481,6 +754,16 @@ int eks_forward(int64_t B, int64_t T, int n, int r, const double *y, const doubl
   if (B < 0 || T < 1) return set_err(EKS_ERR_ARG, "eks_forward: need B >= 0, T >= 1");
   if (B == 0) return EKS_OK;
   hipStream_t s = (hipStream_t)stream;
+  if (n > kMaxObs) {  // 5+ cameras: one wave per trajectory, the solve in LDS
+    if (n > kMaxObsRt) return set_err(EKS_ERR_UNSUPPORTED, "eks_forward: n=%d > %d", n, kMaxObsRt);
+    return dispatch_r(r, [&](auto Rc) {
+      constexpr int RR = decltype(Rc)::value;
+      const size_t lds = RtLds(n, RR).total * sizeof(double);
+      hipLaunchKernelGGL((k_forward_dense_rt<RR>), dim3((unsigned)B), dim3(64), lds, s, B, T, n,
+                         y, ev, m0, S0, A, Q, C, R, params_shared, mf, Vf, S, nll, status);
+      return check_launch("k_forward_dense_rt");
+    });
+  }
   return dispatch_r(r, [&](auto Rc) {
     return dispatch_n(n, [&](auto Nc) {
       constexpr int RR = decltype(Rc)::value, NN = decltype(Nc)::value;
@@ -513,6 +796,16 @@ int eks_kalman_dot(int n, int r, int k, const double *x, const double *V, const 
   if (!x || !V || !C || !R || !out) return set_err(EKS_ERR_ARG, "eks_kalman_dot: NULL pointer");
   if (k < 1) return set_err(EKS_ERR_ARG, "eks_kalman_dot: k must be >= 1");
   hipStream_t s = (hipStream_t)stream;
+  if (n > kMaxObs) {
+    if (n > kMaxObsRt) return set_err(EKS_ERR_UNSUPPORTED, "eks_kalman_dot: n=%d > %d", n, kMaxObsRt);
+    return dispatch_r(r, [&](auto Rc) {
+      constexpr int RR = decltype(Rc)::value;
+      const size_t lds = (RtLds(n, 0).total + (size_t)RR * n) * sizeof(double);
+      hipLaunchKernelGGL((k_kalman_dot_rt<RR>), dim3(1), dim3(64), lds, s, n, k, x, V, C, R, out,
+                         status);
+      return check_launch("k_kalman_dot_rt");
+    });
+  }
   return dispatch_r(r, [&](auto Rc) {
     return dispatch_n(n, [&](auto Nc) {
       constexpr int RR = decltype(Rc)::value, NN = decltype(Nc)::value;

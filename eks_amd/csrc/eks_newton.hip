@@ -130,6 +130,107 @@ __global__ __launch_bounds__(64) void k_newton(
   if (status) status[b] = ok ? 0 : EKS_STATUS_SINGULAR;
 }
 
+// The same for any n <= kMaxObsRt (5+ cameras): n is a runtime loop bound,
+// the observation matrix rows (B and B A) are read from global memory (a few
+// KB per model, L1/L2 resident) and the per-step y / 1/ev from the input rows;
+// every sum keeps the order of k_newton, so results equal the compiled kernel.
+template <int R>
+__global__ __launch_bounds__(64) void k_newton_rt(
+    long long B, long long TT, int n, const double *__restrict__ y, const double *__restrict__ ev,
+    const double *__restrict__ mu0g, const double *__restrict__ S0g,
+    const double *__restrict__ Ag, const double *__restrict__ Bg, const double *__restrict__ Eg,
+    int shared, int max_iter, double *__restrict__ q, int32_t *__restrict__ status) {
+  const long long b = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const long long pb = shared ? 0 : b;
+  double A[R][R], Em[R][R], S0[R][R], P[R][R];
+  load_mat<R, R>(Ag + pb * R * R, A);
+  load_mat<R, R>(Eg + pb * R * R, Em);
+  load_mat<R, R>(S0g + pb * R * R, S0);
+  const double *Bm = Bg + pb * (long long)n * R;  // (n, R) row-major
+  bool ok = inverse<R>(S0, P);  // :123
+  const double *yb = y + b * TT * n;
+  const double *eb = ev + b * TT * n;
+  double *qb = q + b * TT * R;
+  double q0[R];
+  load_vec<R>(mu0g + pb * R, q0);
+  store_vec<R>(qb, q0);  // :121
+  for (int it = 0; it < max_iter; ++it) {
+    double qp[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) qp[i] = q0[i];
+    const long long t_begin = TT > 1 ? 1 : 0;
+    for (long long t = t_begin; t < TT; ++t) {
+      const double *et = eb + t * n, *yt = yb + t * n;
+      double AP[R][R], Pp[R][R], Pi[R][R];
+      matmul<R, R, R>(A, P, AP);
+      matmul_nt<R, R, R>(AP, A, Pp);
+#pragma unroll
+      for (int i = 0; i < R; ++i)
+#pragma unroll
+        for (int j = 0; j < R; ++j) Pp[i][j] = Em[i][j] + Pp[i][j];
+      ok = inverse<R>(Pp, Pi) && ok;
+      double S[R][R];
+#pragma unroll
+      for (int i = 0; i < R; ++i)
+#pragma unroll
+        for (int j = 0; j < R; ++j) S[i][j] = 0.0;
+      for (int k = 0; k < n; ++k) {
+        const double v = et[k];
+        ok = ok && (v != 0.0);
+        const double invd = 1.0 / v;
+        double bk[R];
+        load_vec<R>(Bm + k * R, bk);
+#pragma unroll
+        for (int i = 0; i < R; ++i)
+#pragma unroll
+          for (int j = 0; j < R; ++j) S[i][j] = fma(bk[i] * invd, bk[j], S[i][j]);
+      }
+#pragma unroll
+      for (int i = 0; i < R; ++i)
+#pragma unroll
+        for (int j = 0; j < R; ++j) Pp[i][j] = Pi[i][j] + S[i][j];
+      ok = inverse<R>(Pp, P) && ok;
+      // q = A q - ((P B^T) invD) ((B A) q - y), summed over k in order
+      double Aq[R], acc[R];
+      matvec<R, R>(A, qp, Aq);
+#pragma unroll
+      for (int i = 0; i < R; ++i) acc[i] = 0.0;
+      for (int k = 0; k < n; ++k) {
+        double bk[R], ba[R];
+        load_vec<R>(Bm + k * R, bk);
+#pragma unroll
+        for (int j = 0; j < R; ++j) {  // (B A)[k][j]
+          double s = 0.0;
+#pragma unroll
+          for (int u = 0; u < R; ++u) s = fma(bk[u], A[u][j], s);
+          ba[j] = s;
+        }
+        double s = 0.0;
+#pragma unroll
+        for (int j = 0; j < R; ++j) s = fma(ba[j], qp[j], s);
+        const double res = s - yt[k];
+        const double invd = 1.0 / et[k];
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+          double pbt = 0.0;
+#pragma unroll
+          for (int j = 0; j < R; ++j) pbt = fma(P[i][j], bk[j], pbt);
+          acc[i] = fma(pbt * invd, res, acc[i]);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < R; ++i) qp[i] = Aq[i] - acc[i];
+      store_vec<R>(qb + t * R, qp);
+    }
+    if (TT == 1) {
+#pragma unroll
+      for (int i = 0; i < R; ++i) q0[i] = qp[i];
+    }
+  }
+  if (status) status[b] = ok ? 0 : EKS_STATUS_SINGULAR;
+}
+
 }  // namespace eks
 
 using namespace eks;
@@ -146,6 +247,16 @@ extern "C" int eks_newton_filter(int64_t B, int64_t T, int n, int r, const doubl
   if (max_iter < 1) return set_err(EKS_ERR_ARG, "eks_newton_filter: max_iter must be >= 1");
   if (B == 0) return EKS_OK;
   hipStream_t s = (hipStream_t)stream;
+  if (n > kMaxObs) {  // 5+ cameras: the runtime-n kernel
+    if (n > kMaxObsRt)
+      return set_err(EKS_ERR_UNSUPPORTED, "eks_newton_filter: n=%d > %d", n, kMaxObsRt);
+    return dispatch_r(r, [&](auto Rc) {
+      constexpr int RR = decltype(Rc)::value;
+      hipLaunchKernelGGL((k_newton_rt<RR>), dim3(grid_for(B, 64)), dim3(64), 0, s, B, T, n, y, ev,
+                         mu0, S0, A, Bm, E, params_shared, max_iter, q, status);
+      return check_launch("k_newton_rt");
+    });
+  }
   return dispatch_r(r, [&](auto Rc) {
     return dispatch_n(n, [&](auto Nc) {
       constexpr int RR = decltype(Rc)::value, NN = decltype(Nc)::value;

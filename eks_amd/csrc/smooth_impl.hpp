@@ -728,113 +728,9 @@ EKS_DEV void c1_elem_body(const SmoothArgs &a, const ChunkPlan &p) {
   c1_chunk<R, N, E, T, YT, AI, CI, UNI>(a, p, ln.c, ln.b);
 }
 
-// K1 with TWO chunks per lane, c and c + NC2 (NC2 = ceil(NC / 2)), absorbed
-// step-interleaved from y / ev planes.  The r = 3 element build is bound by
-// its per-step chain of dependent FP64 operations at one wave per SIMD (262
-// VGPRs; a second wave per SIMD does not fit without spilling), so a lane
-// carrying two independent chains gives the scheduler the second chain to
-// fill the latency with.  Chunk 0 (the plain filter from the prior) and a
-// short last chunk run the one-chunk body.  Few-trajectory lanes (!UNI).
-template <int R, int N, typename YT, int AI, int CI>
-__global__ __launch_bounds__(kBlock) void k_c1_elem2(SmoothArgs a, ChunkPlan p) {
-  using T = YevIn<YT>;
-  const long long B = a.B, TT = a.T, NC = p.NC, L = p.L, NC2 = (NC + 1) / 2;
-  const long long lane = blockIdx.x * (long long)kBlock + threadIdx.x;
-  if (lane >= NC2 * B) return;
-  const long long c1 = lane / B, c2 = c1 + NC2;
-  const unsigned b = (unsigned)(lane - c1 * B);
-  const bool pair = c2 < NC && !(c1 == 0 && a.t_base == 0) && (c2 + 1) * L <= TT;
-  if (!pair) {
-    c1_chunk<R, N, 0, T, YT, AI, CI, false>(a, p, c1, b);
-    if (c2 < NC) c1_chunk<R, N, 0, T, YT, AI, CI, false>(a, p, c2, b);
-    return;
-  }
-  Model<R, N> md;
-  md.load(a.params + (long long)b * ParamLayout<R, N>::len, false);
-  const long long s1 = c1 * L, s2 = c2 * L;
-  Elem<R> E1, E2;
-  E1.set_identity();
-  E2.set_identity();
-  NllAcc acc1, acc2;
-  bool ok = true;
-  constexpr int DY = 2;  // L is a multiple of 8
-  YT y1[DY][N], y2[DY][N];
-  double e1[DY][N], e2[DY][N];
-  auto fetch = [&](int q, long long i) {  // unconditional (i clamped by the caller)
-#pragma unroll
-    for (int j = 0; j < N; ++j) {
-      y1[q][j] = pl((const YT *)p.ysrc, (s1 + i) * N + j, p.yB, p.ylane(b));
-      e1[q][j] = pl((const double *)p.evsrc, (s1 + i) * N + j, p.yB, p.ylane(b));
-      y2[q][j] = pl((const YT *)p.ysrc, (s2 + i) * N + j, p.yB, p.ylane(b));
-      e2[q][j] = pl((const double *)p.evsrc, (s2 + i) * N + j, p.yB, p.ylane(b));
-    }
-  };
-#pragma unroll
-  for (int q = 0; q < DY; ++q) fetch(q, q);
-  for (long long i0 = 0; i0 < L; i0 += DY) {
-#pragma unroll
-    for (int q = 0; q < DY; ++q) {
-      double ya[N], ra[N], yb[N], rb[N];
-#pragma unroll
-      for (int j = 0; j < N; ++j) {
-        ya[j] = (double)y1[q][j] - md.off[j];
-        ra[j] = e1[q][j];
-        yb[j] = (double)y2[q][j] - md.off[j];
-        rb[j] = e2[q][j];
-      }
-      fetch(q, min(i0 + q + DY, L - 1));
-      elem_absorb<R, N, AI, CI>(E1, md.A, md.Q, md.C, ya, ra, ok, &acc1);
-      elem_absorb<R, N, AI, CI>(E2, md.A, md.Q, md.C, yb, rb, ok, &acc2);
-    }
-  }
-  if (p.nll_closed) {
-    pl((double *)(a.ws + p.nllp_off), c1, B, b) = acc1.value((double)L * N);
-    pl((double *)(a.ws + p.nllp_off), c2, B, b) = acc2.value((double)L * N);
-  }
-  double *el = (double *)(a.ws + p.elem_off) + (long long)b * NC * Elem<R>::len;
-  E1.store(el + c1 * Elem<R>::len, 1);
-  E2.store(el + c2 * Elem<R>::len, 1);
-  if (!ok) flag(a.status, b, EKS_STATUS_SCAN);
-}
-
-// two chunks per K1 lane (k_c1_elem2) for the r = 3 y / ev sweeps: EKS_C1_PAIR=1.
-// Measured slower at config 5 (K1 1.76 vs 1.60 ms, tools/c5_pair.sh): the pair
-// kernel needs 305 VGPRs (one wave per SIMD) while the one-chunk kernel fits
-// 200 (two waves), and two waves hide the chain latency better than two
-// chains in one wave.  Off by default.
-inline bool c1_pairs() {
-  static const bool v = [] {
-    const char *e = getenv("EKS_C1_PAIR");
-    return e ? atoi(e) != 0 : false;
-  }();
-  return v;
-}
-
 template <int R, int N, int E, typename T, typename YT, int AI, int CI, bool UNI>
 __global__ __launch_bounds__(kBlock) void k_c1_elem(SmoothArgs a, ChunkPlan p) {
   c1_elem_body<R, N, E, T, YT, AI, CI, UNI>(a, p);
-}
-
-// The same with at least W waves per SIMD (VGPRs <= 512 / W).  The r = 3
-// element build from y / ev planes (the shared-member sweep of config 5)
-// needs ~230-280 VGPRs unconstrained, i.e. ONE wave per SIMD, and its
-// per-step chain of dependent scalar updates is then latency bound.
-template <int R, int N, int E, typename T, typename YT, int AI, int CI, bool UNI, int W>
-__global__ __launch_bounds__(kBlock, W) void k_c1_elem_occ(SmoothArgs a, ChunkPlan p) {
-  c1_elem_body<R, N, E, T, YT, AI, CI, UNI>(a, p);
-}
-
-// waves per SIMD of k_c1_elem_occ (EKS_C1_WPE=2: tuning experiments; default
-// 0 = the unconstrained kernel.  Config 5, tools/c5_sweep.sh: 2 waves/SIMD
-// (256 VGPRs) ran as fast as 1 (262), 3 (168, spilling) 2.9x slower.  Since
-// the unconditional y / ev ring loads the unconstrained kernel itself fits in
-// 200 VGPRs (2 waves); forcing 3 spills 46 registers)
-inline int c1_waves_per_simd() {
-  static const int v = [] {
-    const char *e = getenv("EKS_C1_WPE");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
 }
 
 template <int R, int N>
@@ -1697,20 +1593,8 @@ int launch_shape(const SmoothArgs &a, int algo, long long L) {
       auto k1 = [&](auto Ec) {
         constexpr int EE = decltype(Ec)::value;
         prof_mark(a.stream, "k_c1_elem");
-        if constexpr (R == 3 && is_yev<Tp>::value) {
-          if (!U && c1_pairs())
-            hipLaunchKernelGGL((k_c1_elem2<R, N, YT, AI, CI>), dim3(grid_for((p.NC + 1) / 2 * a.B, kBlock)),
-                               dim3(kBlock), 0, a.stream, a, p);
-          else if (c1_waves_per_simd() == 2)
-            hipLaunchKernelGGL((k_c1_elem_occ<R, N, EE, Tp, YT, AI, CI, U, 2>), dim3(gch),
-                               dim3(kBlock), 0, a.stream, a, p);
-          else
-            hipLaunchKernelGGL((k_c1_elem<R, N, EE, Tp, YT, AI, CI, U>), dim3(gch), dim3(kBlock),
-                               0, a.stream, a, p);
-        } else {
-          hipLaunchKernelGGL((k_c1_elem<R, N, EE, Tp, YT, AI, CI, U>), dim3(gch), dim3(kBlock), 0,
-                             a.stream, a, p);
-        }
+        hipLaunchKernelGGL((k_c1_elem<R, N, EE, Tp, YT, AI, CI, U>), dim3(gch), dim3(kBlock), 0,
+                           a.stream, a, p);
         return check_launch("k_c1_elem");
       };
       if constexpr (is_yev<Tp>::value)

@@ -75,7 +75,8 @@ constexpr int fine_len3(int r, int n) { return reg_steps3(r, n) + lds_steps3(r, 
 #endif
 
 struct Plan3 {
-  long long L = 16, NCf = 0, NCc = 0, ng = 0, units = 0;
+  // NCc / units: k3_bwd's 4-chunk units; NCu / units_f: k3_fwd's (4 x FPW)
+  long long L = 16, NCf = 0, NCc = 0, NCu = 0, ng = 0, units = 0, units_f = 0;
   // sync block (zeroed every call): ticket counters (own 128-byte lines),
   // then one flag word per unit for each pass
   size_t sync_bytes = 0, flag1_off = 0, flag2_off = 0;
@@ -87,10 +88,13 @@ inline Plan3 make_plan3(long long B, long long T, int r, int n) {
   p.L = fine_len3(r, n);
   p.NCf = (T + p.L - 1) / p.L;
   p.NCc = (p.NCf + kWV - 1) / kWV;
+  const int kpu = kWV * (r <= 2 ? 2 : 1);  // k3_fwd's fine chunks per unit (fwd_fpw)
+  p.NCu = (p.NCf + kpu - 1) / kpu;
   p.ng = (B + 63) / 64;
   p.units = p.NCc * p.ng;
+  p.units_f = p.NCu * p.ng;
   p.flag1_off = 256;
-  p.flag2_off = p.flag1_off + (size_t)p.units * 4;
+  p.flag2_off = p.flag1_off + (size_t)p.units_f * 4;
   p.sync_bytes = align256(p.flag2_off + (size_t)p.units * 4);
   size_t off = p.sync_bytes;
   auto take = [&](size_t bytes) {
@@ -99,9 +103,9 @@ inline Plan3 make_plan3(long long B, long long T, int r, int n) {
     return o;
   };
   const size_t Bz = (size_t)B;
-  // start state of fine chunk f (f = 1 .. 4 NCc; entry 4 c is also the state
-  // k3_fwd's chain hands from coarse chunk c-1 to c)
-  p.fst_off = take((size_t)(kWV * p.NCc + 1) * state_len(r) * Bz * 8);
+  // start state of fine chunk f (f >= 1; entry KPU c is also the state
+  // k3_fwd's chain hands from its unit c-1 to c)
+  p.fst_off = take((size_t)(std::max(kWV * p.NCc, kpu * p.NCu) + 1) * state_len(r) * Bz * 8);
   // smoothed mean at the first step of coarse chunk c (k3_bwd's chain)
   p.inc2_off = take((size_t)p.NCc * r * Bz * 8);
   p.nllp_off = take((size_t)p.NCf * Bz * 8);
@@ -131,7 +135,14 @@ EKS_DEV void publish_flag(unsigned *flag, int lane) {
 }
 // wait for a flag (the whole wave polls the one word); false on timeout
 // (~0.1 s: only a bug could get there, and then the call must still end)
+#ifndef EKS_K3B_HEAD
+#define EKS_K3B_HEAD 1  // k3_bwd: the next unit's start state / first steps loaded ahead (0: at its start)
+#endif
+#ifndef EKS_K3_NOWAIT
+#define EKS_K3_NOWAIT 0  // 1: tuning experiment only -- skip the chain waits (wrong results)
+#endif
 EKS_DEV bool wait_flag(const unsigned *flag) {
+  if (EKS_K3_NOWAIT) return true;
   unsigned spins = 0;
   while (__hip_atomic_load((k3_gu32 *)flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
     if (++spins > (1u << 16)) return false;
@@ -223,16 +234,23 @@ struct SrcOf<E, N, YevIn<YT>, D> {
   using type = YevRing<N, YT, D>;
 };
 
-// Feed the steps [s, e) of one lane (e - s <= LF) to absorb(t, y - offset, rv).
-// Full chunks run a compile-time loop whose prefetches are unconditional (a
-// load under a lane-divergent `if` is merged into its ring slot by a copy
-// that waits for it, i.e. no prefetch at all); the clamped tail re-reads the
-// last step (a cache hit) instead of branching.
+// The first D steps of a lane's chunk into the ring (issued ahead: for the
+// next unit while the current one finishes its tail).
+template <int D, typename Src>
+EKS_DEV void prefetch_head(Src &src, long long s, long long e) {
+#pragma unroll
+  for (int q = 0; q < D; ++q) src.fetch(q, min(s + q, e - 1));
+}
+
+// Feed the steps [s, e) of one lane (e - s <= LF; the ring's head loaded by
+// prefetch_head) to absorb(t, y - offset, rv).  Full chunks run a
+// compile-time loop whose prefetches are unconditional (a load under a
+// lane-divergent `if` is merged into its ring slot by a copy that waits for
+// it, i.e. no prefetch at all); the clamped tail re-reads the last step (a
+// cache hit) instead of branching.
 template <int LF, int D, int N, typename Src, typename F>
 EKS_DEV void stream_steps(Src &src, long long s, long long e, const double (&off)[N], F &&absorb) {
   if (e - s == LF) {
-#pragma unroll
-    for (int q = 0; q < D; ++q) src.fetch(q, s + q);
 #pragma unroll 1
     for (int i0 = 0; i0 < LF; i0 += D) {
 #pragma unroll
@@ -249,9 +267,6 @@ EKS_DEV void stream_steps(Src &src, long long s, long long e, const double (&off
       }
     }
   } else {
-#pragma unroll
-    for (int q = 0; q < D; ++q)
-      if (s + q < e) src.fetch(q, s + q);
     for (long long t0 = s; t0 < e; t0 += D) {
 #pragma unroll
       for (int q = 0; q < D; ++q) {
@@ -288,15 +303,23 @@ unsigned persistent_grid(long long units) {
 }
 
 // ---------------------------------------------------------------------------
-// k3_fwd: filtering elements + the forward chain (filtered states)
+// k3_fwd: filtering elements + the forward chain (filtered states).  A unit
+// is KPU = 4 x FPW fine chunks: each wave streams FPW consecutive ones (two
+// at r = 2: 128-step units, half the chain links and half the per-unit tail
+// of a one-chunk wave; r = 3 elements are too large for that LDS).
 // ---------------------------------------------------------------------------
+template <int R>
+constexpr int fwd_fpw() { return R <= 2 ? 2 : 1; }
+
 template <int R, int N, int E, typename T, int AI, int CI>
 __global__ __launch_bounds__(64 * kWV) void k3_fwd(SmoothArgs a, Plan3 p) {
   constexpr int EL = Elem<R>::len, KS = R + Sym<R>::len;
   constexpr int D = EKS_K3_D;
   constexpr int LF = fine_len3(R, N);
-  __shared__ double shE[kWV][EL][64];  // fine elements, then prefix compositions
-  __shared__ double shS[KS][64];       // filtered state entering the coarse chunk
+  constexpr int FPW = fwd_fpw<R>(), KPU = kWV * FPW;
+  __shared__ double shA[FPW > 1 ? kWV : 1][EL][64];  // each wave's first element (FPW = 2)
+  __shared__ double shX[kWV][EL][64];  // each wave's element, then prefix compositions
+  __shared__ double shS[KS][64];       // filtered state entering the unit
   __shared__ unsigned tk[2];
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63;
   const long long B = a.B, TT = a.T;
@@ -304,28 +327,53 @@ __global__ __launch_bounds__(64 * kWV) void k3_fwd(SmoothArgs a, Plan3 p) {
   unsigned *flags = (unsigned *)(a.ws + p.flag1_off);
   double *fst = (double *)(a.ws + p.fst_off);
   const double *prm = (const double *)(a.ws + p.prm_off);
+  typename SrcOf<E, N, T, D>::type src;  // member ring, persists across units
+  Model<R, N> md;
+  // model + the first member steps of unit tt (structure checked by k_model_planes)
+  auto head = [&](unsigned tt) {
+    if (tt >= (unsigned long long)p.units_f) return;
+    const long long c = tt / p.ng, g = tt - c * p.ng, ff = (c * kWV + w) * FPW;
+    const unsigned bb = (unsigned)(g * 64 + l);
+    if ((long long)bb < B && ff < p.NCf) {
+      load_model_pl<R, N, AI, CI>(prm, B, bb, ff == 0, md);
+      src.init(a, bb);
+      const long long s = ff * p.L;
+      prefetch_head<D>(src, s, min(TT, s + p.L));
+    }
+  };
+  auto load_state_sh = [&](double (&m)[R], double (&P)[R][R]) {
+    int k = 0;
+#pragma unroll
+    for (int i = 0; i < R; ++i) m[i] = shS[k++][l];
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+#pragma unroll
+      for (int j = i; j < R; ++j) P[i][j] = P[j][i] = shS[k++][l];
+  };
   if (threadIdx.x == 0) tk[0] = atomicAdd(ctr, 1u);
   __syncthreads();
   unsigned t = tk[0];
-  for (int it = 0; t < (unsigned long long)p.units; ++it) {
+  head(t);
+  for (int it = 0; t < (unsigned long long)p.units_f; ++it) {
     unsigned tnext = 0;
-    if (threadIdx.x == 0) tnext = atomicAdd(ctr, 1u);  // consumed at the end of the unit
-    const long long cc = t / p.ng, grp = t - cc * p.ng;
-    const long long f = cc * kWV + w;
+    if (threadIdx.x == 0) tnext = atomicAdd(ctr, 1u);  // consumed after the streaming
+    const long long cu = t / p.ng, grp = t - cu * p.ng;
+    const long long f0 = (cu * kWV + w) * FPW;  // the wave's first fine chunk
     const unsigned b = (unsigned)(grp * 64 + l);
     const bool lane_ok = (long long)b < B;
-    const bool live = lane_ok && f < p.NCf;
+    const bool live = lane_ok && f0 < p.NCf;
     bool ok = true, okf = true;  // element / composition, and the plain filter of chunk 0
-    Elem<R> El;
+    Elem<R> El;                  // the wave's last element (E_B), or its only one
     El.set_identity();
+    if constexpr (FPW > 1) El.store(&shA[w][0][l], 64);  // E_A of a dead wave / lane
     if (live) {
-      Model<R, N> md;  // structure checked by k_model_planes
-      load_model_pl<R, N, AI, CI>(prm, B, b, f == 0, md);
-      const long long s = f * p.L, e = min(TT, s + p.L);
-      typename SrcOf<E, N, T, D>::type src;
-      src.init(a, b);
-      if (f == 0) {  // the first chunk: the plain filter from the prior,
-                     // summarised as the known filtered state (Ab = 0)
+      const long long s0 = f0 * p.L, e0 = min(TT, s0 + FPW * p.L);
+      auto absorb_el = [&](long long, const double (&y)[N], const double (&rv)[N]) {
+        elem_absorb<R, N, AI, CI>(El, md.A, md.Q, md.C, y, rv, ok);
+      };
+      if (f0 == 0) {  // the first chunk: the plain filter from the prior,
+                      // summarised as the known filtered state (Ab = 0)
+        const long long e = min(TT, s0 + p.L);
         double m[R], P[R][R];
         NllAcc acc;
 #pragma unroll
@@ -334,7 +382,7 @@ __global__ __launch_bounds__(64 * kWV) void k3_fwd(SmoothArgs a, Plan3 p) {
 #pragma unroll
           for (int j = 0; j < R; ++j) P[i][j] = md.S0[i][j];
         }
-        stream_steps<LF, D, N>(src, s, e, md.off,
+        stream_steps<LF, D, N>(src, s0, e, md.off,
                                [&](long long tt, const double (&y)[N], const double (&rv)[N]) {
                                  if (tt > 0) kf_predict<R, AI>(m, P, md.A, md.Q);
                                  kf_update<R, N, CI>(m, P, md.C, y, rv, acc, okf);
@@ -348,42 +396,77 @@ __global__ __launch_bounds__(64 * kWV) void k3_fwd(SmoothArgs a, Plan3 p) {
             El.Cb[i][j] = P[i][j];
           }
         }
+        if constexpr (FPW > 1) {
+          El.store(&shA[w][0][l], 64);
+          El.set_identity();
+          if (e0 > e) {
+            prefetch_head<D>(src, e, e0);
+            stream_steps<LF, D, N>(src, e, e0, md.off, absorb_el);
+          }
+        }
+      } else if constexpr (FPW > 1) {
+        // both chunks as one stream; the first element is parked in LDS at
+        // the boundary (a wave-uniform branch once per 16 steps)
+        const long long sb = s0 + p.L;
+        stream_steps<FPW * LF, D, N>(src, s0, e0, md.off,
+                                     [&](long long tt, const double (&y)[N], const double (&rv)[N]) {
+                                       if (tt == sb) {
+                                         El.store(&shA[w][0][l], 64);
+                                         El.set_identity();
+                                       }
+                                       absorb_el(tt, y, rv);
+                                     });
+        if (e0 <= sb) {  // no second chunk (the trajectory ends in the first)
+          El.store(&shA[w][0][l], 64);
+          El.set_identity();
+        }
       } else {
-        stream_steps<LF, D, N>(src, s, e, md.off,
-                               [&](long long, const double (&y)[N], const double (&rv)[N]) {
-                                 elem_absorb<R, N, AI, CI>(El, md.A, md.Q, md.C, y, rv, ok);
-                               });
+        stream_steps<LF, D, N>(src, s0, e0, md.off, absorb_el);
       }
     }
-    El.store(&shE[w][0][l], 64);
+    // X_w = the wave's elements composed (own LDS data: no barrier needed)
+    if constexpr (FPW > 1) {
+      Elem<R> Ea, Et;
+      Ea.load(&shA[w][0][l], 64);
+      ok = compose_elem<R>(Ea, El, Et) && ok;
+      Et.store(&shX[w][0][l], 64);
+    } else {
+      El.store(&shX[w][0][l], 64);
+    }
+    if (threadIdx.x == 0) tk[(it + 1) & 1] = tnext;
     __syncthreads();
-    // prefix compositions (dead chunks / lanes hold the identity, which
-    // composes exactly): round 1 E01 -> slot 1, E23 -> slot 3
+    const unsigned tn = tk[(it + 1) & 1];
+    // the next unit's first member steps in flight during this unit's tail
+    // (wave 0 after its chain wait: vmcnt counts in order, so a prefetch
+    // issued before the poll would hold the poll back until it lands)
+    if (w != 0) head(tn);
+    // prefix over the waves (dead chunks / lanes hold the identity, which
+    // composes exactly): round 1 X01 -> slot 1, X23 -> slot 3
     if (w == 1 || w == 3) {
       Elem<R> Ea, Eb, Et;
-      Ea.load(&shE[w - 1][0][l], 64);
-      Eb.load(&shE[w][0][l], 64);
+      Ea.load(&shX[w - 1][0][l], 64);
+      Eb.load(&shX[w][0][l], 64);
       ok = compose_elem<R>(Ea, Eb, Et) && ok;
-      Et.store(&shE[w][0][l], 64);
+      Et.store(&shX[w][0][l], 64);
     }
     __syncthreads();
-    // round 2: E012 -> slot 2 (wave 2); the coarse element E0123 (wave 0)
+    // round 2: X012 -> slot 2 (wave 2); the unit's element X0123 (wave 0)
     Elem<R> Ec;
     if (w == 2) {
       Elem<R> Ea, Eb, Et;
-      Ea.load(&shE[1][0][l], 64);
-      Eb.load(&shE[2][0][l], 64);
+      Ea.load(&shX[1][0][l], 64);
+      Eb.load(&shX[2][0][l], 64);
       ok = compose_elem<R>(Ea, Eb, Et) && ok;
-      Et.store(&shE[2][0][l], 64);
+      Et.store(&shX[2][0][l], 64);
     } else if (w == 0) {
       Elem<R> Ea, Eb;
-      Ea.load(&shE[1][0][l], 64);
-      Eb.load(&shE[3][0][l], 64);
+      Ea.load(&shX[1][0][l], 64);
+      Eb.load(&shX[3][0][l], 64);
       ok = compose_elem<R>(Ea, Eb, Ec) && ok;
     }
     if (w == 0) {
-      // the chain: filtered state entering coarse chunk cc, published by the
-      // unit of chunk cc-1 (for cc = 0 any state: chunk 0's element has Ab = 0)
+      // the chain: filtered state entering unit cu, published by the unit
+      // before it (for cu = 0 any state: chunk 0's element has Ab = 0)
       double m[R], P[R][R];
 #pragma unroll
       for (int i = 0; i < R; ++i) {
@@ -391,11 +474,11 @@ __global__ __launch_bounds__(64 * kWV) void k3_fwd(SmoothArgs a, Plan3 p) {
 #pragma unroll
         for (int j = 0; j < R; ++j) P[i][j] = 0.0;
       }
-      if (cc > 0) {
-        if (!wait_flag(flags + (cc - 1) * p.ng + grp)) ok = false;
+      if (cu > 0) {
+        if (!wait_flag(flags + (cu - 1) * p.ng + grp)) ok = false;
         if (lane_ok) {
           int k = 0;
-          const long long pl0 = (cc * kWV) * KS;
+          const long long pl0 = (cu * KPU) * KS;
 #pragma unroll
           for (int i = 0; i < R; ++i) m[i] = ld_wt(&pl(fst, pl0 + (k++), B, b));
 #pragma unroll
@@ -413,11 +496,11 @@ __global__ __launch_bounds__(64 * kWV) void k3_fwd(SmoothArgs a, Plan3 p) {
 #pragma unroll
           for (int j = i; j < R; ++j) shS[k++][l] = P[i][j];
       }
-      ok = compose_state<R>(m, P, Ec) && ok;  // the state leaving coarse chunk cc
-      if (cc + 1 < p.NCc) {
+      ok = compose_state<R>(m, P, Ec) && ok;  // the state leaving unit cu
+      if (cu + 1 < p.NCu) {
         if (lane_ok) {
           int k = 0;
-          const long long pl0 = ((cc + 1) * kWV) * KS;
+          const long long pl0 = ((cu + 1) * KPU) * KS;
 #pragma unroll
           for (int i = 0; i < R; ++i) st_wt(&pl(fst, pl0 + (k++), B, b), m[i]);
 #pragma unroll
@@ -425,31 +508,37 @@ __global__ __launch_bounds__(64 * kWV) void k3_fwd(SmoothArgs a, Plan3 p) {
 #pragma unroll
             for (int j = i; j < R; ++j) st_wt(&pl(fst, pl0 + (k++), B, b), P[i][j]);
         }
-        publish_flag(flags + cc * p.ng + grp, l);
+        publish_flag(flags + cu * p.ng + grp, l);
       }
+      head(tn);
     }
     __syncthreads();
-    // waves 1-3: the start state of their fine chunk = the entering state
-    // composed with the elements before it (slots 0 / 1 / 2 = E0 / E01 / E012)
-    if (w >= 1 && live) {
+    // fine start states: wave w's first chunk starts from the entering state
+    // composed with the waves before it (slots 0 / 1 / 2 = X0 / X01 / X012;
+    // wave 0's is the entering state itself, stored by the unit before), its
+    // second from that composed with its first element
+    if (live) {
       double m[R], P[R][R];
-      int k = 0;
-#pragma unroll
-      for (int i = 0; i < R; ++i) m[i] = shS[k++][l];
-#pragma unroll
-      for (int i = 0; i < R; ++i)
-#pragma unroll
-        for (int j = i; j < R; ++j) P[i][j] = P[j][i] = shS[k++][l];
-      Elem<R> Ep;
-      Ep.load(&shE[w - 1][0][l], 64);
-      ok = compose_state<R>(m, P, Ep) && ok;
-      store_state_pl<R>(fst, f * KS, B, b, m, P);
+      load_state_sh(m, P);
+      if (w >= 1) {
+        Elem<R> Ep;
+        Ep.load(&shX[w - 1][0][l], 64);
+        ok = compose_state<R>(m, P, Ep) && ok;
+        store_state_pl<R>(fst, f0 * KS, B, b, m, P);
+      }
+      if constexpr (FPW > 1) {
+        if (f0 + 1 < p.NCf) {
+          Elem<R> Ea;
+          Ea.load(&shA[w][0][l], 64);
+          ok = compose_state<R>(m, P, Ea) && ok;
+          store_state_pl<R>(fst, (f0 + 1) * KS, B, b, m, P);
+        }
+      }
     }
     if (lane_ok)
       flag(a.status, b, (ok ? 0 : EKS_STATUS_SCAN) | (okf ? 0 : EKS_STATUS_SINGULAR));
-    if (threadIdx.x == 0) tk[(it + 1) & 1] = tnext;
-    __syncthreads();  // LDS free for the next unit, its ticket visible
-    t = tk[(it + 1) & 1];
+    __syncthreads();  // LDS free for the next unit
+    t = tn;
   }
 }
 
@@ -474,9 +563,37 @@ __global__ __launch_bounds__(64 * kWV) void k3_bwd(SmoothArgs a, Plan3 p) {
   const double *prm = (const double *)(a.ws + p.prm_off);
   const bool vec2 = N == 2 && a.oj == 1 && ((a.ob | a.ot) & 1) == 0 &&
                     (((uintptr_t)a.out) & 15) == 0;
+  typename SrcOf<E, N, T, D>::type src;  // member ring, persists across units
+  double m[R], P[R][R];                  // filtered state (the start state of a unit ahead)
+  // start state + the first member steps of unit tt (the model itself is
+  // loaded at the unit's start: the backward sweep of the current unit still
+  // needs the current one)
+  auto head = [&](unsigned tt) {
+    if (tt >= (unsigned long long)p.units) return;
+    const long long c = p.NCc - 1 - (long long)(tt / p.ng), g = tt - (tt / p.ng) * p.ng;
+    const long long ff = c * kWV + w;
+    const unsigned bb = (unsigned)(g * 64 + l);
+    if ((long long)bb < B && ff < p.NCf) {
+      using L = ParamLayout<R, N>;
+      if (ff == 0) {
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+          m[i] = pl(prm, L::m0 + i, B, bb);
+#pragma unroll
+          for (int j = 0; j < R; ++j) P[i][j] = pl(prm, L::S0 + i * R + j, B, bb);
+        }
+      } else {
+        load_state_pl<R>(fst, ff * KS, B, bb, m, P);
+      }
+      src.init(a, bb);
+      const long long s = ff * p.L;
+      prefetch_head<D>(src, s, min(TT, s + p.L));
+    }
+  };
   if (tid == 0) tk[0] = atomicAdd(ctr, 1u);
   __syncthreads();
   unsigned t = tk[0];
+  if (EKS_K3B_HEAD) head(t);
   for (int it = 0; t < (unsigned long long)p.units; ++it) {
     unsigned tnext = 0;
     if (tid == 0) tnext = atomicAdd(ctr, 1u);
@@ -493,23 +610,8 @@ __global__ __launch_bounds__(64 * kWV) void k3_bwd(SmoothArgs a, Plan3 p) {
     Mp.set_identity();
     const long long s = f * p.L, e = min(TT, s + p.L);
     if (live) {
-      load_model_pl<R, N, AI, CI>(prm, B, b, f == 0, md);
-      double m[R], P[R][R];
-      if (f == 0) {
-#pragma unroll
-        for (int i = 0; i < R; ++i) {
-          m[i] = md.m0[i];
-#pragma unroll
-          for (int j = 0; j < R; ++j) P[i][j] = md.S0[i][j];
-        }
-      } else {
-        load_state_pl<R>(fst, f * KS, B, b, m, P);
-      }
-      typename SrcOf<E, N, T, D>::type src;
-      src.init(a, b);
-#pragma unroll
-      for (int q = 0; q < D; ++q)
-        if (s + q < e) src.fetch(q, s + q);
+      if (!EKS_K3B_HEAD) head(t);  // start state + first member steps at the unit start
+      load_model_pl<R, N, AI, CI>(prm, B, b, false, md);
       NllAcc acc;
 #pragma unroll
       for (int i = 0; i < LF; ++i) {
@@ -578,7 +680,12 @@ __global__ __launch_bounds__(64 * kWV) void k3_bwd(SmoothArgs a, Plan3 p) {
 #pragma unroll
       for (int u = 0; u < R; ++u) shM[w - 1][k++][l] = Mp.g[u];
     }
+    if (tid == 0) tk[(it + 1) & 1] = tnext;
     __syncthreads();
+    const unsigned tn = tk[(it + 1) & 1];
+    // the next unit's start state and first member steps in flight (wave 0
+    // after its chain, as in k3_fwd)
+    if (EKS_K3B_HEAD && w != 0) head(tn);
     double ms[R];  // smoothed mean at the first step after this chunk
     if (w == 0) {
       // the chain: the mean at the first step of coarse chunk cc+1, published
@@ -629,6 +736,7 @@ __global__ __launch_bounds__(64 * kWV) void k3_bwd(SmoothArgs a, Plan3 p) {
           for (int u = 0; u < R; ++u) st_wt(&pl(inc, cc * R + u, B, b), x[u]);
         publish_flag(flags + cc * p.ng + grp, l);
       }
+      if (EKS_K3B_HEAD) head(tn);
     }
     __syncthreads();
     if (w >= 1)
@@ -715,9 +823,8 @@ __global__ __launch_bounds__(64 * kWV) void k3_bwd(SmoothArgs a, Plan3 p) {
     }
     if (lane_ok)
       flag(a.status, b, (ok ? 0 : EKS_STATUS_SINGULAR) | (okc ? 0 : EKS_STATUS_SCAN));
-    if (tid == 0) tk[(it + 1) & 1] = tnext;
-    __syncthreads();  // LDS free for the next unit, its ticket visible
-    t = tk[(it + 1) & 1];
+    __syncthreads();  // LDS free for the next unit
+    t = tn;
   }
 }
 
@@ -755,7 +862,7 @@ int launch_algo3(const SmoothArgs &a) {
     if ((rc = check_launch("k_model_planes"))) return rc;
     prof_mark(a.stream, "k3_fwd");
     hipLaunchKernelGGL((k3_fwd<R, N, EE, Tp, AI, CI>),
-                       dim3(persistent_grid<k3_fwd<R, N, EE, Tp, AI, CI>>(p.units)), dim3(64 * kWV), 0,
+                       dim3(persistent_grid<k3_fwd<R, N, EE, Tp, AI, CI>>(p.units_f)), dim3(64 * kWV), 0,
                        a.stream, a, p);
     if ((rc = check_launch("k3_fwd"))) return rc;
     prof_mark(a.stream, "k3_bwd");

@@ -28,17 +28,25 @@ def shard_range(total: int, world: int, rank: int):
     return lo, lo + base + (1 if rank < extra else 0)
 
 
-def init(backend: str | None = None):
-    """Initialise torch.distributed when WORLD_SIZE > 1 (127.0.0.1 rendezvous
-    from torchrun's MASTER_ADDR/PORT)."""
+def init(backend: str | None = None, force: bool = False):
+    """Initialise torch.distributed when WORLD_SIZE > 1 (or ``force``: a
+    one-rank group, e.g. to run the RCCL code paths on one GPU), 127.0.0.1
+    rendezvous from torchrun's MASTER_ADDR/PORT.  With nccl (= RCCL) the rank
+    is bound to its GPU (LOCAL_RANK) before the group is created and the
+    device is handed to the group (``device_id``), so the communicator and
+    every barrier use that device instead of a guess."""
     import torch.distributed as dist
     rank, world, local = env_world()
-    if world > 1 and not dist.is_initialized():
+    if (world > 1 or force) and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        import torch
         if backend is None:
-            import torch
             backend = "nccl" if torch.cuda.is_available() else "gloo"
-        dist.init_process_group(backend=backend, rank=rank, world_size=world)
+        kw = {}
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            kw["device_id"] = torch.device("cuda", local)
+        dist.init_process_group(backend=backend, rank=rank, world_size=world, **kw)
     return rank, world, local
 
 

@@ -82,3 +82,31 @@ def test_cpu_task_kinds_match_oracle_smoothers():
     cams = [st_m[:, :, 2 * c:2 * c + 2] for c in range(3)]
     np.testing.assert_allclose(outs[1], O.multicam_smooth(cams, 0.01, 25.0)[0], rtol=0, atol=1e-9)
     np.testing.assert_array_equal(outs[2], O.singleview_smooth(tasks[2][1], 0.01, 25.0)[0])
+
+
+def test_multi_rank_line_schema(tmp_path, monkeypatch):
+    """An N > 1 line (the driver's SCALE runs) carries the CPU baseline (rank
+    0's shard), the PMC traffic of one rank's launch (looked up by the
+    per-rank shard key, i.e. the entry an N = 1 run of that shard size
+    wrote), the distributed block and the timed RCCL gather."""
+    import json
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "8"])
+    a = bench.parse()
+    assert bench.runs_cpu_baseline(0, a) and not bench.runs_cpu_baseline(1, a)
+    key = "config4-singleview-v128-k17-e5-t10000-a3"
+    pmc = tmp_path / "bench_pmc.json"
+    pmc.write_text(json.dumps({"entries": {key: {"hbm_bytes_per_launch": 2.5e9}}}))
+    w = dict(key=key, desc="config 4 shard", cfg=dict(videos=1024, trajectories_per_rank=2176),
+             bytes_per_unit=56, units=2176 * 10000)
+    cpu = dict(value=1e5, unit="kp-ts/s", cores=16, kind="port", sample="...")
+    line = bench.make_line(a, w, 8, 3, 2176 * 10000, 17408 * 10000, 0.01 * a.steps,
+                           [("k3_fwd", 0.2), ("k3_bwd", 0.3)], 0.5, cpu, 1e-11, None, None,
+                           3.2, 2.79e9, 1.0, True, "nccl", pmc_path=str(pmc))
+    assert line["n_gpus"] == 8 and line["scaling"] == "strong"
+    assert line["cpu_baseline"] is cpu
+    assert line["roofline"]["traffic"] == 2.5e9
+    assert line["distributed"]["world_size"] == 8 and line["distributed"]["backend"] == "nccl"
+    assert line["gather_ms"] == 3.2 and line["gather_bytes"] == 2.79e9
+    assert line["value"] == 17408 * 10000 / 0.01
+    # the N = 1 line of the full batch looks up its own entry
+    assert bench.load_pmc("config4-singleview-v1024-k17-e5-t10000-a3", str(pmc)) is None

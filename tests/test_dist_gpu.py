@@ -71,3 +71,49 @@ def test_two_ranks_gathered_equal_one_rank():
         assert p.exitcode == 0
     assert shape == (VIDEOS, T, K, 2)
     assert equal, f"sharded outputs differ from the 1-rank batch by {diff}"
+
+
+def _rccl_worker(port, q):
+    import torch
+    from eks_amd import dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1",
+                      LOCAL_RANK="0")
+    try:
+        dist.init(backend="nccl", force=True)     # RCCL, bound to cuda:0 (device_id)
+        import torch.distributed as td
+        backend = str(td.get_backend())
+        dev = torch.device("cuda", 0)
+        loc = torch.arange(3 * 5 * 2, dtype=torch.float64, device=dev).view(3, 5, 2)
+        full = dist.gather_to_rank0(loc, 3)       # the padded device-tensor gather branch
+        tmax = dist.max_over_ranks(2.5, device=dev)
+        tsum = dist.sum_over_ranks(7.0, device=dev)
+        dist.barrier()
+        q.put((backend, full.is_cuda, bool(torch.equal(full, loc)), tmax, tsum))
+    except Exception as exc:  # report, do not hang the parent
+        q.put(("error", repr(exc)))
+    finally:
+        import torch.distributed as td
+        if td.is_initialized():
+            td.destroy_process_group()
+
+
+def test_rccl_world1_collectives():
+    """The nccl (= RCCL on ROCm) code paths of eks_amd.dist on one GPU: a
+    world_size-1 group bound to cuda:0 runs the padded device-tensor
+    gather_to_rank0 (what bench.py's N > 1 gather issues), max_over_ranks,
+    sum_over_ranks and barrier through RCCL."""
+    import torch
+    import torch.multiprocessing as mp
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(_free_port(), q))
+    p.start()
+    res = q.get(timeout=240)
+    p.join(timeout=60)
+    assert res[0] == "nccl", res
+    assert p.exitcode == 0
+    _, on_gpu, equal, tmax, tsum = res
+    assert on_gpu and equal
+    assert tmax == 2.5 and tsum == 7.0

@@ -1,15 +1,18 @@
 """Parity at BASELINE.json's full config-4 size (1024 videos x 17 keypoints
-x 5 members x 10 000 frames, 1.74e8 keypoint-timesteps) through properties
-that do not need the CPU oracle (which would take hours at this size):
+x 5 members x 10 000 frames, 1.74e8 keypoint-timesteps):
 
+* the CPU oracle (oracle/eks_oracle.py singleview_smooth: ensemble ->
+  single-view fit -> filtering_pass -> smooth_backward -> projection, the
+  reference's recursions restated) on 8 trajectories spread over the whole
+  batch at full T = 10 000 (a few seconds of numpy) against the GPU fit +
+  smooth of the whole batch: algo 3 (the default here) and algo 2 within
+  1e-5 px (BASELINE.json's tolerance);
 * the time-parallel algorithms (algo 2, 16 chunks per trajectory; algo 3,
   625 chunks of 16 frames) equal the sequential recursion (algo 1) on every
   trajectory (max|d| < 1e-8 px);
 * translation equivariance: shifting every member by (dx, dy) shifts the
   model offsets and the smoothed outputs by exactly that (to rounding);
-* the device fit + hand-off path equals fit + smooth on the members.
-The CPU oracle itself is compared on a sample of this workload by bench.py
-(`max_abs_diff_vs_cpu`)."""
+* the device fit + hand-off path equals fit + smooth on the members."""
 import numpy as np
 import pytest
 
@@ -29,6 +32,28 @@ def work():
     params, _ = batch.fit(obs, kind="singleview", n=2, r=2, smooth_param=0.01,
                           quantile_keep=25)
     return torch, obs_tm, obs, params
+
+
+# 8 trajectories spread over the 17 408 of the batch (first, last, and
+# keypoints of videos in between)
+ORACLE_SAMPLE = (0, 2175, 4351, 6530, 8703, 10884, 13059, 17407)
+
+
+def test_oracle_sample_full_size(work):
+    torch, obs_tm, obs, params = work
+    from eks_amd import _lib, batch
+    from oracle import eks_oracle as O
+    flags = _lib.EKS_MODEL_A_IDENTITY | _lib.EKS_MODEL_C_IDENTITY
+    B, T = obs.shape[0], obs.shape[1]
+    assert _lib.load().eks_smooth_algo(B, T, 2, 2, 5, 0) == 3
+    outs = {algo: batch.smooth(obs, params, n=2, r=2, algo=algo, flags=flags, check=True)["out"]
+            for algo in (0, 2)}
+    for b in ORACLE_SAMPLE:
+        st = obs_tm[..., b].permute(1, 0, 2).double().cpu().numpy()   # (E, T, 2)
+        ref, _, _ = O.singleview_smooth(st, 0.01, 25)
+        for algo, out in outs.items():
+            d = float(np.abs(out[b].cpu().numpy() - ref).max())
+            assert d < 1e-5, (b, algo, d)
 
 
 def test_algo2_equals_sequential_full_size(work):

@@ -464,7 +464,7 @@ def test_newton_golden(torch, path):
 
 
 @pytest.mark.parametrize("r,n,shared", [(1, 1, 0), (2, 2, 1), (3, 4, 0), (3, 8, 1), (4, 5, 0),
-                                        (6, 8, 0), (5, 3, 1)])
+                                        (6, 8, 0), (5, 3, 1), (3, 10, 0), (3, 12, 1), (2, 64, 0)])
 def test_newton_batch_vs_oracle(torch, r, n, shared):
     from eks_amd.newton_eks import newton_filter_batch
     from oracle import eks_oracle as O
@@ -515,6 +515,54 @@ def test_opti_multicam_golden(torch):
     out = np.concatenate([dfs[f"{c}_df"].to_numpy()[:, :2] for c in cams], axis=1)
     assert np.abs(out - g["golden"]).max() < OUT_TOL
     assert np.isnan(dfs["top_df"].to_numpy()[:, 2]).all()
+
+
+def test_opti_multicam_five_cameras_golden(torch):
+    """eks_opti_smoother_multi_cam with 5 cameras (n = 10: the runtime-n
+    Newton filter) against the reference run on the same synthetic members
+    (tools/gen_golden.py bign)."""
+    from eks_amd.multiview_pca_smoother import eks_opti_smoother_multi_cam
+    g = np.load(os.path.join(GOLDEN, "opti_multicam_V5.npz"))
+    st = g["stack"]                                    # (E, T, 2V)
+    E, V = st.shape[0], st.shape[2] // 2
+    cams = [f"cam{c}" for c in range(V)]
+    by_cam = [[pd.DataFrame(st[e][:, 2 * c:2 * c + 2], columns=["paw_x", "paw_y"])
+               for e in range(E)] for c in range(V)]
+    dfs = eks_opti_smoother_multi_cam(by_cam, "paw", float(g["s"]), float(g["q"]), cams)
+    out = np.concatenate([dfs[f"{c}_df"].to_numpy()[:, :2] for c in cams], axis=1)
+    assert np.abs(out - g["out"]).max() < OUT_TOL
+
+
+@pytest.mark.parametrize("n", [16, 64])
+def test_forward_runtime_n_vs_oracle(torch, n):
+    """The runtime-n dense forward and kalman_dot (n > 8: one wave per
+    trajectory, the n x n solve in LDS) against the oracle at n = 16 and at
+    the n = 64 maximum, with exact-agreement frames (ev = 0)."""
+    from eks_amd import core
+    from oracle import eks_oracle as O
+    rng = np.random.default_rng(n)
+    r, T = 3, 120
+    A = np.eye(r) + 0.05 * rng.normal(size=(r, r))
+    M = rng.normal(size=(r, r))
+    Q = M @ M.T / r + 0.5 * np.eye(r)
+    S0 = 20 * np.eye(r)
+    C = rng.normal(size=(n, r)) * 2.0
+    x = np.cumsum(rng.normal(size=(T, r)), axis=0)
+    y = x @ C.T + rng.normal(size=(T, n))
+    ev = rng.uniform(0.05, 4.0, size=(T, n))
+    ev[rng.random(size=T) < 0.2, 0] = 0.0
+    m0 = rng.normal(size=r)
+    mf, Vf, S = core.filtering_pass(y, m0, S0, C, np.eye(n), A, Q, ev)
+    mo, Vo, So = O.filtering_pass(y, m0, S0, C, np.eye(n), A, Q, ev)
+    _close(mf, mo)
+    _close(Vf, Vo)
+    _close(S, So)
+    ms, _, _ = core.smooth_backward(y, mf, Vf, S, A, Q, C)
+    mso, _, _ = O.smooth_backward(y, mo, Vo, So, A)
+    _close(ms, mso)
+    v = rng.normal(size=(n, r))
+    _close(core.kalman_dot(v, S0, C, np.diag(ev[1])), O.kalman_dot(v, S0, C, np.diag(ev[1])),
+           rtol=1e-10)
 
 
 def test_opti_pupil_golden(torch):

@@ -455,8 +455,71 @@ def gen_paw(mv, ut):
     print("  wrote paw fixtures")
 
 
+def gen_bign(ek, mv):
+    """Observation dimensions above the compiled kernels' n <= 8 (5 and 6
+    cameras: n = 10, 12): filtering_pass / smooth_backward / kalman_dot, the
+    Newton filter, and eks_opti_smoother_multi_cam on 5 synthetic cameras."""
+    import eks.newton_eks as ne
+    cases = [(3, 10, 3, "rand"), (3, 10, 257, "rand"), (3, 12, 257, "rand"),
+             (3, 10, 300, "zero_var")]
+    for i, (r, n, T, kind) in enumerate(cases):
+        rng = np.random.default_rng(5000 + i)
+        A = np.eye(r) + 0.05 * rng.normal(size=(r, r))
+        Q = _spd(rng, r, 0.5)
+        S0 = _spd(rng, r, 20.0)
+        m0 = rng.normal(size=r)
+        C = rng.normal(size=(n, r)) * 2.0
+        x = np.cumsum(rng.normal(size=(T, r)), axis=0)
+        y = x @ C.T + rng.normal(size=(T, n))
+        ev = rng.uniform(0.05, 4.0, size=(T, n))
+        if kind == "zero_var":
+            rows = np.where(rng.random(size=T) < 0.2)[0]
+            ev[rows, rng.integers(0, n, size=len(rows))] = 0.0
+        R_in = np.eye(n)
+        R = R_in.copy()
+        mf, Vf, S = ek.filtering_pass(y, m0, S0, C, R, A, Q, ev)
+        ms, Vs, CV = ek.smooth_backward(y, mf, Vf, S, A, Q, C)
+        vec = rng.normal(size=n)
+        mat = rng.normal(size=(n, r))
+        kd_vec = ek.kalman_dot(vec, S0, C, np.diag(ev[0]))
+        kd_mat = ek.kalman_dot(mat, S0, C, np.diag(ev[0]))
+        _save(f"core_{kind}_r{r}_n{n}_T{T}", y=y, m0=m0, S0=S0, C=C, R_in=R_in, A=A, Q=Q,
+              ev=ev, mf=mf, Vf=Vf, S=S, ms=ms, Vs=Vs, CV=CV, R_out=R,
+              kd_vec_in=vec, kd_mat_in=mat, kd_vec=kd_vec, kd_mat=kd_mat)
+    for i, (r, n, T, it) in enumerate([(3, 10, 200, 1), (3, 12, 100, 2)]):
+        rng = np.random.default_rng(6000 + i)
+        A = np.eye(r) + 0.05 * rng.normal(size=(r, r))
+        E = _spd(rng, r, 0.5)
+        S0 = _spd(rng, r, 20.0)
+        mu0 = rng.normal(size=r)
+        B = rng.normal(size=(n, r)) * 2.0
+        x = np.cumsum(rng.normal(size=(T, r)), axis=0)
+        y = x @ B.T + rng.normal(size=(T, n))
+        ev = rng.uniform(0.05, 4.0, size=(T, n))
+        res = ne.kalman_newton_recursive(y, mu0, S0, A, B, ev, E, max_iter=it)
+        q = res if it == 1 else res[0]
+        _save(f"newton_r{r}_n{n}_T{T}_it{it}", y=y, mu0=mu0, S0=S0, A=A, B=B, ev=ev, E=E,
+              max_iter=it, q=q)
+    # eks_opti_smoother_multi_cam with V = 5 cameras (n = 10), E = 4 members
+    V, E, T = 5, 4, 300
+    st = synthetic.multiview_obs(np.random.default_rng(6100), V, E, T, K=1)[:, :, 0, :]
+    st = st.astype(np.float64)                                   # (E, T, 2V)
+    cams = [f"cam{c}" for c in range(V)]
+    kp = "paw"
+    by_cam = [[pd.DataFrame(st[e][:, 2 * c:2 * c + 2], columns=[f"{kp}_x", f"{kp}_y"])
+               for e in range(E)] for c in range(V)]
+    dfs = mv.eks_opti_smoother_multi_cam(by_cam, kp, 0.01, 25, cams, plot=False)
+    out = np.concatenate(
+        [dfs[f"{cam}_df"].loc[:, ("ensemble-kalman_tracker", kp, c)].to_numpy()[:, None]
+         for cam in cams for c in ("x", "y")], axis=1)
+    _save("opti_multicam_V5", stack=st, s=0.01, q=25.0, out=out)
+
+
 def main():
     ek, mv, ps, ut = _import_reference()
+    if len(sys.argv) > 1 and sys.argv[1] == "bign":
+        gen_bign(ek, mv)
+        return
     if len(sys.argv) > 1 and sys.argv[1] == "paw":
         gen_paw(mv, ut)
         return
@@ -475,6 +538,7 @@ def main():
     gen_newton(mv, ps, ut)
     gen_cli(mv, ps, ut)
     gen_paw(mv, ut)
+    gen_bign(ek, mv)
 
 
 if __name__ == "__main__":

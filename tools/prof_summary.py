@@ -1,6 +1,6 @@
 """Summarise a tools/gpu_profile.sh run into profiles/<tag>/.
 
-    python tools/prof_summary.py gpurun_out/prof_r01 profiles/r01 [workload_key, e.g. config4-singleview-v1024-k17-e5-t10000-n1-strong-a0]
+    python tools/prof_summary.py gpurun_out/prof_r01 profiles/r01 [workload_key, e.g. config4-singleview-v1024-k17-e5-t10000-a3]
 
 Reads the rocprofv3 kernel-stats CSV and the FETCH_SIZE / WRITE_SIZE counter
 CSVs (separate passes), keeps the EKS kernels, and writes
@@ -9,8 +9,10 @@ CSVs (separate passes), keeps the EKS kernels, and writes
   profiles/<tag>/summary.json          per-kernel average duration and HBM
                                        bytes per launch (FETCH_SIZE x 2 on
                                        gfx950 + WRITE_SIZE, both in KiB)
-and, if a workload key is given, bench_pmc.json at the repository root for
-bench.py (outside profiles/, which does not travel to the GPU box).
+and, if a workload key is given, that key's entry of bench_pmc.json at the
+repository root for bench.py (outside profiles/, which does not travel to
+the GPU box).  Keys name one rank's launch (its shard of the workload), so
+an N-rank bench line reads the entry of an N = 1 run of the same shard.
 """
 from __future__ import annotations
 
@@ -74,10 +76,17 @@ def main(src: str, dst: str, key: str | None = None):
                         "kernel's designed byte count.")
     json.dump(summary, open(os.path.join(dst, "summary.json"), "w"), indent=1)
     if key:
-        pm = {"workload_key": key, "hbm_bytes_per_launch": tot_bytes,
-              "source": os.path.join(dst, "summary.json"), "kernels": summary["kernels"]}
         root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-        json.dump(pm, open(os.path.join(root, "bench_pmc.json"), "w"), indent=1)
+        path = os.path.join(root, "bench_pmc.json")
+        try:
+            allpm = json.load(open(path))
+        except Exception:
+            allpm = {}
+        entries = allpm.get("entries") or {}
+        entries[key] = {"hbm_bytes_per_launch": tot_bytes, "kernel_ms": tot_ms,
+                        "source": os.path.join(dst, "summary.json"),
+                        "kernels": summary["kernels"]}
+        json.dump({"entries": entries}, open(path, "w"), indent=1)
     print(json.dumps(summary["per_call"]))
     for k, d in summary["kernels"].items():
         print(f"  {k:40s} {d.get('avg_ms', 0):8.3f} ms  {d['hbm_bytes'] / 1e9:7.3f} GB  "
