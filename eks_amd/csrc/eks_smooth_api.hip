@@ -103,6 +103,9 @@ static int smooth_call(const void *obs, int obs_dtype, int64_t B, int64_t T, int
   if (!workspace || workspace_bytes < need)
     return set_err(EKS_ERR_ARG, "eks_smooth: workspace of %zu bytes needed", need);
   if (al == 3 && !out) al = 2;  // filter only: algo 3 has no NLL-only mode
+  // algo 3 addresses members as unsigned 32-bit offsets within a step
+  if (al == 3 && (sb < 0 || se < 0 || sj < 0 || ((int64_t)(E - 1) * se + (int64_t)(n - 1) * sj) * 8 >= (1LL << 31)))
+    al = 2;
   hipStream_t s = (hipStream_t)stream;
   if (phase <= 1 && hipMemsetAsync(status, 0, (size_t)B * sizeof(int32_t), s) != hipSuccess)
     return set_err(EKS_ERR_HIP, "eks_smooth: hipMemsetAsync(status) failed");

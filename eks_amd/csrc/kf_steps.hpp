@@ -11,6 +11,7 @@
 // The host promises the structure and the kernels verify it per trajectory
 // (status bit EKS_STATUS_BAD_MODEL on violation).
 #pragma once
+#include <type_traits>
 #include "eks_common.hpp"
 #include "small_linalg.hpp"
 
@@ -93,8 +94,34 @@ EKS_DEV bool is_pupil_c(const double (&M)[N][R]) {
 // Ensemble reduction of one step (E members x N coordinates in registers).
 // Same arithmetic as ensemble_reduce (numpy order, exact divisions).
 // ---------------------------------------------------------------------------
+// min / max of floats as one v_med3_f32 each: med3(a, b, -inf) = min(a, b).
+// The infinities go through an empty asm so the compiler cannot turn the med3
+// back into a v_min/v_max, which in IEEE mode costs a canonicalisation of
+// every input (NaN members are handled by the caller's flag, not here).
+struct F32MinMax {
+  float ninf = -__builtin_inff(), pinf = __builtin_inff();
+  EKS_DEV F32MinMax() {
+    asm volatile("" : "+s"(ninf));
+    asm volatile("" : "+s"(pinf));
+  }
+  EKS_DEV float mn(float a, float b) const { return __builtin_amdgcn_fmed3f(a, b, ninf); }
+  EKS_DEV float mx(float a, float b) const { return __builtin_amdgcn_fmed3f(a, b, pinf); }
+};
+
 template <int E, typename T>
 EKS_DEV void median_of(const T (&raw)[E], double &med) {
+  if constexpr (std::is_same<T, float>::value && (E == 3 || E == 5)) {
+    // exact selections (one of the members): 1 / 7 v_med3_f32
+    if constexpr (E == 3) {
+      med = (double)__builtin_amdgcn_fmed3f(raw[0], raw[1], raw[2]);
+    } else {
+      const F32MinMax f;
+      const float lo = f.mx(f.mn(raw[0], raw[1]), f.mn(raw[2], raw[3]));
+      const float hi = f.mn(f.mx(raw[0], raw[1]), f.mx(raw[2], raw[3]));
+      med = (double)__builtin_amdgcn_fmed3f(lo, hi, raw[4]);
+    }
+    return;
+  }
   T s[E];
 #pragma unroll
   for (int e = 0; e < E; ++e) s[e] = raw[e];
@@ -238,6 +265,14 @@ struct NllAcc {
   }
 };
 
+// the same interface, accumulating nothing (smoothing calls without an NLL
+// output: no per-step likelihood arithmetic)
+struct NoAcc {
+  EKS_DEV void add(double, double, double) {}
+  EKS_DEV void renorm() {}
+  EKS_DEV double value(double) const { return 0.0; }
+};
+
 // ---------------------------------------------------------------------------
 // Pupil measurement rows (eks/pupil_smoother.py:150-153, PUPIL_KEYS order:
 // top x, y, bottom x, y, right x, y, left x, y; state (diameter, com_x,
@@ -268,8 +303,9 @@ EKS_DEV double cdot3(double x0, double x1, double x2) {
 //   y = (r2 y1 + r1 y2) / (r1 + r2),  r = r1 r2 / (r1 + r2),
 // i.e. one scalar observation plus a state-free NLL term (added to `acc`).
 // r1 + r2 = 0 (both exact) is the reference's singular S.
+template <typename Acc>
 EKS_DEV void merge_obs(double y1, double r1, double y2, double r2, double &y, double &r,
-                       NllAcc *acc, bool &ok) {
+                       Acc *acc, bool &ok) {
   const double sr = r1 + r2;
   ok = ok && !(sr <= 0.0);
   const double inv = rcp_nr(sr);
@@ -279,8 +315,8 @@ EKS_DEV void merge_obs(double y1, double r1, double y2, double r2, double &y, do
 }
 
 // one scalar update of the filter state with pupil row H (kf_update's body)
-template <int H0, int H1, int H2>
-EKS_DEV void kf_update_row(double (&m)[3], double (&P)[3][3], double y, double rv, NllAcc &acc,
+template <int H0, int H1, int H2, typename Acc = NllAcc>
+EKS_DEV void kf_update_row(double (&m)[3], double (&P)[3][3], double y, double rv, Acc &acc,
                            bool &ok) {
   double v[3];
 #pragma unroll
@@ -307,20 +343,20 @@ EKS_DEV void kf_update_row(double (&m)[3], double (&P)[3][3], double y, double r
 
 // Measurement update with diagonal R, one scalar observation at a time
 // (algebraically the reference's kalman_dot with the n x n solve).
-template <int R, int N, int CI>
+template <int R, int N, int CI, typename Acc = NllAcc>
 EKS_DEV void kf_update(double (&m)[R], double (&P)[R][R], const double (&C)[N][R],
-                       const double (&y)[N], const double (&rv)[N], NllAcc &acc, bool &ok) {
+                       const double (&y)[N], const double (&rv)[N], Acc &acc, bool &ok) {
   if constexpr (CI == kCPupil) {
     static_assert(R == 3 && N == 8, "the pupil model is r = 3, n = 8");
     double ya, ra, yb, rb;
     merge_obs(y[0], rv[0], y[2], rv[2], ya, ra, &acc, ok);
     merge_obs(y[5], rv[5], y[7], rv[7], yb, rb, &acc, ok);
-    kf_update_row<0, 2, 0>(m, P, ya, ra, acc, ok);
-    kf_update_row<-1, 0, 2>(m, P, y[1], rv[1], acc, ok);
-    kf_update_row<1, 0, 2>(m, P, y[3], rv[3], acc, ok);
-    kf_update_row<1, 2, 0>(m, P, y[4], rv[4], acc, ok);
-    kf_update_row<0, 0, 2>(m, P, yb, rb, acc, ok);
-    kf_update_row<-1, 2, 0>(m, P, y[6], rv[6], acc, ok);
+    kf_update_row<0, 2, 0, Acc>(m, P, ya, ra, acc, ok);
+    kf_update_row<-1, 0, 2, Acc>(m, P, y[1], rv[1], acc, ok);
+    kf_update_row<1, 0, 2, Acc>(m, P, y[3], rv[3], acc, ok);
+    kf_update_row<1, 2, 0, Acc>(m, P, y[4], rv[4], acc, ok);
+    kf_update_row<0, 0, 2, Acc>(m, P, yb, rb, acc, ok);
+    kf_update_row<-1, 2, 0, Acc>(m, P, y[6], rv[6], acc, ok);
     acc.renorm();
     return;
   }

@@ -135,9 +135,6 @@ EKS_DEV void publish_flag(unsigned *flag, int lane) {
 }
 // wait for a flag (the whole wave polls the one word); false on timeout
 // (~0.1 s: only a bug could get there, and then the call must still end)
-#ifndef EKS_K3B_HEAD
-#define EKS_K3B_HEAD 1  // k3_bwd: the next unit's start state / first steps loaded ahead (0: at its start)
-#endif
 #ifndef EKS_K3_NOWAIT
 #define EKS_K3_NOWAIT 0  // 1: tuning experiment only -- skip the chain waits (wrong results)
 #endif
@@ -154,29 +151,51 @@ EKS_DEV bool wait_flag(const unsigned *flag) {
 
 // Step sources of the two member passes: a D-deep register ring of raw step
 // data, reduced to (raw average, variance) on use.
+// Raw buffer loads of the members: the step's base address goes into the
+// buffer descriptor (scalar, advanced per step), member e / coordinate j's
+// offset into soffset (scalar) and the trajectory's into a 32-bit voffset:
+// no vector address arithmetic per load.  launch_algo3 slices the batch so
+// that voffset + soffset stays below 2^32 (the descriptor's range).
+EKS_DEV __amdgpu_buffer_rsrc_t member_rsrc(const void *p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, -1, 0x00020000);
+}
+template <typename T>
+EKS_DEV T member_load(__amdgpu_buffer_rsrc_t rs, unsigned voff, int soff) {
+  constexpr int aux = EKS_NT_LOAD ? 2 : 0;  // nt: streamed once
+  if constexpr (sizeof(T) == 4)
+    return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(rs, voff, soff, aux));
+  else
+    return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, aux));
+}
+
 template <int E, int N, typename T, int D>
 struct MemberRing {
   T v[D][E][N];
-  const T *ob;
-  long long st, se, sj;
+  const char *base;  // uniform
+  unsigned loff;     // trajectory b's byte offset
+  long long stb;     // bytes per step
+  int seb, sjb;      // bytes per member / coordinate
   bool median;
-  EKS_DEV void init(const SmoothArgs &a, unsigned b) {
-    ob = (const T *)a.obs + (long long)b * a.sb;
-    st = a.st;
-    se = a.se;
-    sj = a.sj;
+  // the uniform fields once, outside any lane-dependent branch (a value
+  // merged at a divergent join is divergent to the compiler: the buffer
+  // descriptor would need a waterfall loop per load)
+  EKS_DEV void init(const SmoothArgs &a) {
+    base = (const char *)a.obs;
+    stb = a.st * (long long)sizeof(T);
+    seb = (int)(a.se * (long long)sizeof(T));
+    sjb = (int)(a.sj * (long long)sizeof(T));
     median = a.median != 0;
+    loff = 0;
+  }
+  EKS_DEV void lane(const SmoothArgs &a, unsigned b) {
+    loff = (unsigned)((unsigned long long)b * (unsigned long long)a.sb * sizeof(T));
   }
   EKS_DEV void fetch(int slot, long long t) {
-#if EKS_NT_LOAD
-    const T *p = ob + t * st;
+    const __amdgpu_buffer_rsrc_t rs = member_rsrc(base + t * stb);
 #pragma unroll
     for (int e = 0; e < E; ++e)
 #pragma unroll
-      for (int j = 0; j < N; ++j) v[slot][e][j] = __builtin_nontemporal_load(p + e * se + j * sj);
-#else
-    load_step<E, N, T>(ob + t * st, se, sj, v[slot]);
-#endif
+      for (int j = 0; j < N; ++j) v[slot][e][j] = member_load<T>(rs, loff, e * seb + j * sjb);
   }
   EKS_DEV void get(int slot, double (&avg)[N], double (&rv)[N]) const {
 #pragma unroll
@@ -198,12 +217,13 @@ struct YevRing {
   const double *eb;
   long long B;
   unsigned b;
-  EKS_DEV void init(const SmoothArgs &a, unsigned bb) {
+  EKS_DEV void init(const SmoothArgs &a) {
     yb = (const YT *)a.obs;
     eb = (const double *)((const char *)a.obs + yev_ev_offset(a.B, a.T, N, sizeof(YT)));
     B = a.B;
-    b = bb;
+    b = 0;
   }
+  EKS_DEV void lane(const SmoothArgs &, unsigned bb) { b = bb; }
   EKS_DEV void fetch(int slot, long long t) {
 #pragma unroll
     for (int j = 0; j < N; ++j) {
@@ -328,15 +348,19 @@ __global__ __launch_bounds__(64 * kWV) void k3_fwd(SmoothArgs a, Plan3 p) {
   double *fst = (double *)(a.ws + p.fst_off);
   const double *prm = (const double *)(a.ws + p.prm_off);
   typename SrcOf<E, N, T, D>::type src;  // member ring, persists across units
+  src.init(a);
   Model<R, N> md;
-  // model + the first member steps of unit tt (structure checked by k_model_planes)
+  // model + the first member steps of unit tt (structure checked by
+  // k_model_planes).  Lanes past the last trajectory read trajectory 0 (their
+  // results are never stored): every branch here is wave-uniform.
   auto head = [&](unsigned tt) {
     if (tt >= (unsigned long long)p.units_f) return;
     const long long c = tt / p.ng, g = tt - c * p.ng, ff = (c * kWV + w) * FPW;
     const unsigned bb = (unsigned)(g * 64 + l);
-    if ((long long)bb < B && ff < p.NCf) {
-      load_model_pl<R, N, AI, CI>(prm, B, bb, ff == 0, md);
-      src.init(a, bb);
+    const unsigned bl = (long long)bb < B ? bb : 0u;
+    if (ff < p.NCf) {
+      load_model_pl<R, N, AI, CI>(prm, B, bl, ff == 0, md);
+      src.lane(a, bl);
       const long long s = ff * p.L;
       prefetch_head<D>(src, s, min(TT, s + p.L));
     }
@@ -352,7 +376,7 @@ __global__ __launch_bounds__(64 * kWV) void k3_fwd(SmoothArgs a, Plan3 p) {
   };
   if (threadIdx.x == 0) tk[0] = atomicAdd(ctr, 1u);
   __syncthreads();
-  unsigned t = tk[0];
+  unsigned t = __builtin_amdgcn_readfirstlane(tk[0]);  // uniform: every index below in SGPRs
   head(t);
   for (int it = 0; t < (unsigned long long)p.units_f; ++it) {
     unsigned tnext = 0;
@@ -365,8 +389,8 @@ __global__ __launch_bounds__(64 * kWV) void k3_fwd(SmoothArgs a, Plan3 p) {
     bool ok = true, okf = true;  // element / composition, and the plain filter of chunk 0
     Elem<R> El;                  // the wave's last element (E_B), or its only one
     El.set_identity();
-    if constexpr (FPW > 1) El.store(&shA[w][0][l], 64);  // E_A of a dead wave / lane
-    if (live) {
+    if constexpr (FPW > 1) El.store(&shA[w][0][l], 64);  // E_A of a dead wave
+    if (f0 < p.NCf) {  // (dead lanes: trajectory 0's data, replaced by the identity below)
       const long long s0 = f0 * p.L, e0 = min(TT, s0 + FPW * p.L);
       auto absorb_el = [&](long long, const double (&y)[N], const double (&rv)[N]) {
         elem_absorb<R, N, AI, CI>(El, md.A, md.Q, md.C, y, rv, ok);
@@ -424,6 +448,11 @@ __global__ __launch_bounds__(64 * kWV) void k3_fwd(SmoothArgs a, Plan3 p) {
         stream_steps<LF, D, N>(src, s0, e0, md.off, absorb_el);
       }
     }
+    if (!lane_ok) {  // a dead lane's chain stays exact (identity elements)
+      El.set_identity();
+      if constexpr (FPW > 1) El.store(&shA[w][0][l], 64);
+      ok = okf = true;
+    }
     // X_w = the wave's elements composed (own LDS data: no barrier needed)
     if constexpr (FPW > 1) {
       Elem<R> Ea, Et;
@@ -435,7 +464,7 @@ __global__ __launch_bounds__(64 * kWV) void k3_fwd(SmoothArgs a, Plan3 p) {
     }
     if (threadIdx.x == 0) tk[(it + 1) & 1] = tnext;
     __syncthreads();
-    const unsigned tn = tk[(it + 1) & 1];
+    const unsigned tn = __builtin_amdgcn_readfirstlane(tk[(it + 1) & 1]);
     // the next unit's first member steps in flight during this unit's tail
     // (wave 0 after its chain wait: vmcnt counts in order, so a prefetch
     // issued before the poll would hold the poll back until it lands)
@@ -545,7 +574,7 @@ __global__ __launch_bounds__(64 * kWV) void k3_fwd(SmoothArgs a, Plan3 p) {
 // ---------------------------------------------------------------------------
 // k3_bwd: the final smoothing pass + the backward chain (smoothed means)
 // ---------------------------------------------------------------------------
-template <int R, int N, int E, typename T, int AI, int CI>
+template <int R, int N, int E, typename T, int AI, int CI, bool NLL>
 __global__ __launch_bounds__(64 * kWV) void k3_bwd(SmoothArgs a, Plan3 p) {
   constexpr int KS = R + Sym<R>::len, MP = R * R + R;
   constexpr int D = EKS_K3_D;
@@ -563,37 +592,9 @@ __global__ __launch_bounds__(64 * kWV) void k3_bwd(SmoothArgs a, Plan3 p) {
   const double *prm = (const double *)(a.ws + p.prm_off);
   const bool vec2 = N == 2 && a.oj == 1 && ((a.ob | a.ot) & 1) == 0 &&
                     (((uintptr_t)a.out) & 15) == 0;
-  typename SrcOf<E, N, T, D>::type src;  // member ring, persists across units
-  double m[R], P[R][R];                  // filtered state (the start state of a unit ahead)
-  // start state + the first member steps of unit tt (the model itself is
-  // loaded at the unit's start: the backward sweep of the current unit still
-  // needs the current one)
-  auto head = [&](unsigned tt) {
-    if (tt >= (unsigned long long)p.units) return;
-    const long long c = p.NCc - 1 - (long long)(tt / p.ng), g = tt - (tt / p.ng) * p.ng;
-    const long long ff = c * kWV + w;
-    const unsigned bb = (unsigned)(g * 64 + l);
-    if ((long long)bb < B && ff < p.NCf) {
-      using L = ParamLayout<R, N>;
-      if (ff == 0) {
-#pragma unroll
-        for (int i = 0; i < R; ++i) {
-          m[i] = pl(prm, L::m0 + i, B, bb);
-#pragma unroll
-          for (int j = 0; j < R; ++j) P[i][j] = pl(prm, L::S0 + i * R + j, B, bb);
-        }
-      } else {
-        load_state_pl<R>(fst, ff * KS, B, bb, m, P);
-      }
-      src.init(a, bb);
-      const long long s = ff * p.L;
-      prefetch_head<D>(src, s, min(TT, s + p.L));
-    }
-  };
   if (tid == 0) tk[0] = atomicAdd(ctr, 1u);
   __syncthreads();
-  unsigned t = tk[0];
-  if (EKS_K3B_HEAD) head(t);
+  unsigned t = __builtin_amdgcn_readfirstlane(tk[0]);  // uniform: every index below in SGPRs
   for (int it = 0; t < (unsigned long long)p.units; ++it) {
     unsigned tnext = 0;
     if (tid == 0) tnext = atomicAdd(ctr, 1u);
@@ -609,10 +610,29 @@ __global__ __launch_bounds__(64 * kWV) void k3_bwd(SmoothArgs a, Plan3 p) {
     Affine<R> Mp;       // this chunk's RTS map: ms[s] = G ms[e] + g
     Mp.set_identity();
     const long long s = f * p.L, e = min(TT, s + p.L);
-    if (live) {
-      if (!EKS_K3B_HEAD) head(t);  // start state + first member steps at the unit start
-      load_model_pl<R, N, AI, CI>(prm, B, b, false, md);
-      NllAcc acc;
+    // wave-uniform branch: lanes past the last trajectory run on trajectory
+    // 0's data and store nothing
+    const unsigned bl = lane_ok ? b : 0u;
+    if (f < p.NCf) {
+      load_model_pl<R, N, AI, CI>(prm, B, bl, f == 0, md);
+      double m[R], P[R][R];
+      if (f == 0) {
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+          m[i] = md.m0[i];
+#pragma unroll
+          for (int j = 0; j < R; ++j) P[i][j] = md.S0[i][j];
+        }
+      } else {
+        load_state_pl<R>(fst, f * KS, B, bl, m, P);
+      }
+      typename SrcOf<E, N, T, D>::type src;
+      src.init(a);
+      src.lane(a, bl);
+#pragma unroll
+      for (int q = 0; q < D; ++q)
+        if (s + q < e) src.fetch(q, s + q);
+      typename std::conditional<NLL, NllAcc, NoAcc>::type acc;  // NLL shares only when asked for
 #pragma unroll
       for (int i = 0; i < LF; ++i) {
         const long long tt = s + i;
@@ -623,7 +643,7 @@ __global__ __launch_bounds__(64 * kWV) void k3_bwd(SmoothArgs a, Plan3 p) {
 #pragma unroll
           for (int j = 0; j < N; ++j) y[j] = avg[j] - md.off[j];
           if (tt > 0) kf_predict<R, AI>(m, P, md.A, md.Q);
-          kf_update<R, N, CI>(m, P, md.C, y, rv, acc, ok);
+          kf_update<R, N, CI, decltype(acc)>(m, P, md.C, y, rv, acc, ok);
           double st[KS];
           {
             int k = 0;
@@ -669,7 +689,11 @@ __global__ __launch_bounds__(64 * kWV) void k3_bwd(SmoothArgs a, Plan3 p) {
           }
         }
       }
-      if (a.nll) pl((double *)(a.ws + p.nllp_off), f, B, b) = acc.value((double)(e - s) * N);
+      if (NLL && lane_ok) pl((double *)(a.ws + p.nllp_off), f, B, b) = acc.value((double)(e - s) * N);
+      if (!lane_ok) {
+        ok = true;
+        Mp.set_identity();
+      }
     }
     if (w >= 1) {
       int k = 0;
@@ -680,12 +704,7 @@ __global__ __launch_bounds__(64 * kWV) void k3_bwd(SmoothArgs a, Plan3 p) {
 #pragma unroll
       for (int u = 0; u < R; ++u) shM[w - 1][k++][l] = Mp.g[u];
     }
-    if (tid == 0) tk[(it + 1) & 1] = tnext;
     __syncthreads();
-    const unsigned tn = tk[(it + 1) & 1];
-    // the next unit's start state and first member steps in flight (wave 0
-    // after its chain, as in k3_fwd)
-    if (EKS_K3B_HEAD && w != 0) head(tn);
     double ms[R];  // smoothed mean at the first step after this chunk
     if (w == 0) {
       // the chain: the mean at the first step of coarse chunk cc+1, published
@@ -736,7 +755,6 @@ __global__ __launch_bounds__(64 * kWV) void k3_bwd(SmoothArgs a, Plan3 p) {
           for (int u = 0; u < R; ++u) st_wt(&pl(inc, cc * R + u, B, b), x[u]);
         publish_flag(flags + cc * p.ng + grp, l);
       }
-      if (EKS_K3B_HEAD) head(tn);
     }
     __syncthreads();
     if (w >= 1)
@@ -823,8 +841,9 @@ __global__ __launch_bounds__(64 * kWV) void k3_bwd(SmoothArgs a, Plan3 p) {
     }
     if (lane_ok)
       flag(a.status, b, (ok ? 0 : EKS_STATUS_SINGULAR) | (okc ? 0 : EKS_STATUS_SCAN));
-    __syncthreads();  // LDS free for the next unit
-    t = tn;
+    if (tid == 0) tk[(it + 1) & 1] = tnext;
+    __syncthreads();  // LDS free for the next unit, its ticket visible
+    t = __builtin_amdgcn_readfirstlane(tk[(it + 1) & 1]);
   }
 }
 
@@ -844,7 +863,7 @@ __global__ __launch_bounds__(64) void k3_nll(SmoothArgs a, Plan3 p) {
 
 // host: the launches of one algo-3 call
 template <int R, int N, int AI, int CI>
-int launch_algo3(const SmoothArgs &a) {
+int launch_algo3_one(const SmoothArgs &a) {
   const Plan3 p = make_plan3(a.B, a.T, R, N);
   const bool yev = a.dtype == EKS_YEV32 || a.dtype == EKS_YEV64;
   const bool f32 = a.dtype == EKS_F32;
@@ -866,9 +885,14 @@ int launch_algo3(const SmoothArgs &a) {
                        a.stream, a, p);
     if ((rc = check_launch("k3_fwd"))) return rc;
     prof_mark(a.stream, "k3_bwd");
-    hipLaunchKernelGGL((k3_bwd<R, N, EE, Tp, AI, CI>),
-                       dim3(persistent_grid<k3_bwd<R, N, EE, Tp, AI, CI>>(p.units)), dim3(64 * kWV), 0,
-                       a.stream, a, p);
+    if (a.nll)
+      hipLaunchKernelGGL((k3_bwd<R, N, EE, Tp, AI, CI, true>),
+                         dim3(persistent_grid<k3_bwd<R, N, EE, Tp, AI, CI, true>>(p.units)),
+                         dim3(64 * kWV), 0, a.stream, a, p);
+    else
+      hipLaunchKernelGGL((k3_bwd<R, N, EE, Tp, AI, CI, false>),
+                         dim3(persistent_grid<k3_bwd<R, N, EE, Tp, AI, CI, false>>(p.units)),
+                         dim3(64 * kWV), 0, a.stream, a, p);
     if ((rc = check_launch("k3_bwd"))) return rc;
     if (a.nll) {
       prof_mark(a.stream, "k3_nll");
@@ -892,3 +916,36 @@ int launch_algo3(const SmoothArgs &a) {
   };
   return f32 ? by_e(float{}) : by_e(double{});
 }
+
+// The member loads address trajectory b as a 32-bit byte offset b * sb *
+// sizeof(T) (plus the member / coordinate offset) from the step's base.  A
+// batch whose offsets do not fit (members stored trajectory-major with > 4 GB
+// between the first and last trajectory) runs as consecutive slices on the
+// same stream and workspace: algo 3's results depend on T only, so the
+// slices give the bits of the one-piece call.
+template <int R, int N, int AI, int CI>
+int launch_algo3(const SmoothArgs &a) {
+  const bool yev = a.dtype == EKS_YEV32 || a.dtype == EKS_YEV64;
+  const long long esz = a.dtype == EKS_F32 ? 4 : 8;
+  const long long per = yev ? 0 : a.sb * esz;  // bytes between trajectories
+  // the largest member / coordinate offset of a step (buffer soffset)
+  const long long soff = yev ? 0 : ((a.E - 1) * a.se + (N - 1) * a.sj) * esz + esz;
+  const long long lim = (1LL << 32) - soff;
+  if (per <= 0 || (a.B - 1) * per < lim) return launch_algo3_one<R, N, AI, CI>(a);
+  const long long cap = std::max(1LL, lim / per);  // trajectories per slice
+  if (lim <= 0)
+    return set_err(EKS_ERR_UNSUPPORTED, "eks_smooth algo 3: member strides beyond 4 GB per step");
+  for (long long b0 = 0; b0 < a.B; b0 += cap) {
+    SmoothArgs s = a;
+    s.B = std::min(cap, a.B - b0);
+    s.obs = (const char *)a.obs + b0 * per;
+    s.params = a.params + b0 * ParamLayout<R, N>::len;
+    s.out = a.out + b0 * a.ob;
+    s.ms = a.ms ? a.ms + b0 * a.T * R : nullptr;
+    s.nll = a.nll ? a.nll + b0 : nullptr;
+    s.status = a.status + b0;
+    if (const int rc = launch_algo3_one<R, N, AI, CI>(s)) return rc;
+  }
+  return 0;
+}
+
