@@ -1,10 +1,15 @@
 // Ensemble reduction over E members (eks/ensemble_kalman.py:34-46), in
-// registers.  Matches numpy's arithmetic:
-//   mean = pairwise_sum(x) / E                     (numpy add.reduce order)
-//   var  = sum((x - mean)^2) / E / E               (np.var ddof=0, then / E)
+// registers, the one arithmetic every kernel uses (eks_ensemble, the fit,
+// every smoother), so hand-offs between them are bit-identical:
+//   mean = sum(x) * (1/E)    (numpy's summation order; the division as a
+//                             product by the reciprocal: <= 1 ulp from
+//                             numpy's x / E, exact for E a power of two)
+//   var  = sum((x - mean)^2) * (1/E^2)   (np.var ddof=0, then / E; <= 2 ulp)
 //   median: middle order statistic, or (lo + hi) / 2 for even E
 // and propagates NaN as np.median / np.var do.
 #pragma once
+#include <type_traits>
+
 #include "small_linalg.hpp"
 
 namespace eks {
@@ -51,40 +56,69 @@ EKS_DEV void sort_net(T (&v)[E]) {
     }
 }
 
+// min / max of floats as one v_med3_f32 each: med3(a, b, -inf) = min(a, b).
+// The infinities go through an empty asm so the compiler cannot turn the med3
+// back into a v_min/v_max, which in IEEE mode costs a canonicalisation of
+// every input (NaN members are handled by the caller's flag, not here).
+struct F32MinMax {
+  float ninf = -__builtin_inff(), pinf = __builtin_inff();
+  EKS_DEV F32MinMax() {
+    asm volatile("" : "+s"(ninf));
+    asm volatile("" : "+s"(pinf));
+  }
+  EKS_DEV float mn(float a, float b) const { return __builtin_amdgcn_fmed3f(a, b, ninf); }
+  EKS_DEV float mx(float a, float b) const { return __builtin_amdgcn_fmed3f(a, b, pinf); }
+};
+
+// the median of E member values (exact: a selection, or the mean of the two
+// middle ones for even E)
+template <int E, typename T>
+EKS_DEV double median_of(const T (&raw)[E]) {
+  if constexpr (std::is_same<T, float>::value && (E == 3 || E == 5)) {
+    if constexpr (E == 3) {  // 1 v_med3_f32
+      return (double)__builtin_amdgcn_fmed3f(raw[0], raw[1], raw[2]);
+    } else {  // 7: drop the min and max of s0..s3, then the median of 3
+      const F32MinMax f;
+      const float lo = f.mx(f.mn(raw[0], raw[1]), f.mn(raw[2], raw[3]));
+      const float hi = f.mn(f.mx(raw[0], raw[1]), f.mx(raw[2], raw[3]));
+      return (double)__builtin_amdgcn_fmed3f(lo, hi, raw[4]);
+    }
+  } else {
+    T v[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) v[e] = raw[e];
+    sort_net<E, T>(v);
+    if constexpr (E % 2 == 1)
+      return to_f64(v[E / 2]);
+    else
+      return (to_f64(v[E / 2 - 1]) + to_f64(v[E / 2])) / 2.0;
+  }
+}
+
 // Reduce one column of E member values (compile-time E).
 template <int E, typename T>
 EKS_DEV void ensemble_reduce(const T (&raw)[E], bool median, double &avg, double &var) {
+  constexpr double invE = 1.0 / (double)E, invE2 = 1.0 / ((double)E * (double)E);
   double x[E];
   bool has_nan = false;
 #pragma unroll
   for (int e = 0; e < E; ++e) {
     x[e] = to_f64(raw[e]);
-    has_nan |= (x[e] != x[e]);
+    has_nan |= (raw[e] != raw[e]);
   }
-  const double mean = np_sum<E>(x) / E;
+  const double mean = np_sum<E>(x) * invE;
   double d[E];
 #pragma unroll
   for (int e = 0; e < E; ++e) {
     const double t = x[e] - mean;
     d[e] = t * t;
   }
-  var = np_sum<E>(d) / E / E;
+  var = np_sum<E>(d) * invE2;  // NaN members make it NaN by themselves
   if (median) {
-    T s[E];
-#pragma unroll
-    for (int e = 0; e < E; ++e) s[e] = raw[e];
-    sort_net<E, T>(s);
-    if constexpr (E % 2 == 1) {
-      avg = to_f64(s[E / 2]);
-    } else {
-      avg = (to_f64(s[E / 2 - 1]) + to_f64(s[E / 2])) / 2.0;
-    }
+    avg = median_of<E, T>(raw);
+    if (has_nan) avg = __builtin_nan("");  // the selection would skip them
   } else {
     avg = mean;
-  }
-  if (has_nan) {
-    avg = __builtin_nan("");
-    var = __builtin_nan("");
   }
 }
 
@@ -113,11 +147,13 @@ EKS_DEV void ensemble_reduce_rt(const T *p, long long se, int E, bool median, do
     for (int k = full; k < E; ++k) s += f(k);
     return s;
   };
-  const double mean = np_sum_rt([&](int i) { return to_f64(p[(long long)i * se]); }) / E;
+  // the compiled path's arithmetic (products by the reciprocals)
+  const double invE = 1.0 / (double)E, invE2 = 1.0 / ((double)E * (double)E);
+  const double mean = np_sum_rt([&](int i) { return to_f64(p[(long long)i * se]); }) * invE;
   var = np_sum_rt([&](int i) {
           const double t = to_f64(p[(long long)i * se]) - mean;
           return t * t;
-        }) / E / E;
+        }) * invE2;
   for (int e = 0; e < E; ++e) {
     const double v = to_f64(p[(long long)e * se]);
     has_nan |= (v != v);

@@ -13,6 +13,7 @@
 #pragma once
 #include <type_traits>
 #include "eks_common.hpp"
+#include "ensemble.hpp"
 #include "small_linalg.hpp"
 
 namespace eks {
@@ -90,113 +91,11 @@ EKS_DEV bool is_pupil_c(const double (&M)[N][R]) {
   return ok;
 }
 
-// ---------------------------------------------------------------------------
-// Ensemble reduction of one step (E members x N coordinates in registers).
-// Same arithmetic as ensemble_reduce (numpy order, exact divisions).
-// ---------------------------------------------------------------------------
-// min / max of floats as one v_med3_f32 each: med3(a, b, -inf) = min(a, b).
-// The infinities go through an empty asm so the compiler cannot turn the med3
-// back into a v_min/v_max, which in IEEE mode costs a canonicalisation of
-// every input (NaN members are handled by the caller's flag, not here).
-struct F32MinMax {
-  float ninf = -__builtin_inff(), pinf = __builtin_inff();
-  EKS_DEV F32MinMax() {
-    asm volatile("" : "+s"(ninf));
-    asm volatile("" : "+s"(pinf));
-  }
-  EKS_DEV float mn(float a, float b) const { return __builtin_amdgcn_fmed3f(a, b, ninf); }
-  EKS_DEV float mx(float a, float b) const { return __builtin_amdgcn_fmed3f(a, b, pinf); }
-};
-
-template <int E, typename T>
-EKS_DEV void median_of(const T (&raw)[E], double &med) {
-  if constexpr (std::is_same<T, float>::value && (E == 3 || E == 5)) {
-    // exact selections (one of the members): 1 / 7 v_med3_f32
-    if constexpr (E == 3) {
-      med = (double)__builtin_amdgcn_fmed3f(raw[0], raw[1], raw[2]);
-    } else {
-      const F32MinMax f;
-      const float lo = f.mx(f.mn(raw[0], raw[1]), f.mn(raw[2], raw[3]));
-      const float hi = f.mn(f.mx(raw[0], raw[1]), f.mx(raw[2], raw[3]));
-      med = (double)__builtin_amdgcn_fmed3f(lo, hi, raw[4]);
-    }
-    return;
-  }
-  T s[E];
-#pragma unroll
-  for (int e = 0; e < E; ++e) s[e] = raw[e];
-  if constexpr (E == 3) {
-    const T lo = fmin(s[0], s[1]), hi = fmax(s[0], s[1]);
-    med = (double)fmax(lo, fmin(hi, s[2]));
-  } else if constexpr (E == 5) {
-    // median of 5: drop the min and max of {s0..s3} (never the median of 5),
-    // then the median of the two survivors and s4
-    T a = fmin(s[0], s[1]), b = fmax(s[0], s[1]);
-    T c = fmin(s[2], s[3]), d = fmax(s[2], s[3]);
-    T lo = fmax(a, c);          // second smallest candidate
-    T hi = fmin(b, d);          // second largest candidate
-    T x = s[4];
-    T l2 = fmin(lo, hi), h2 = fmax(lo, hi);
-    med = (double)fmax(l2, fmin(h2, x));
-  } else {
-#pragma unroll
-    for (int p = 0; p < E; ++p)
-#pragma unroll
-      for (int i = p & 1; i + 1 < E; i += 2) {
-        const T a = s[i], b = s[i + 1];
-        s[i] = a < b ? a : b;
-        s[i + 1] = a < b ? b : a;
-      }
-    if constexpr (E % 2 == 1)
-      med = (double)s[E / 2];
-    else
-      med = ((double)s[E / 2 - 1] + (double)s[E / 2]) * 0.5;
-  }
-}
-
+// one ensemble column (E members in registers): the shared reduction of
+// ensemble.hpp
 template <int E, typename T>
 EKS_DEV void ensemble_col(const T (&raw)[E], bool median, double &avg, double &var) {
-  constexpr double dE = (double)E;
-  constexpr double invE = 1.0 / (double)E;
-  double x[E];
-  bool nan = false;
-#pragma unroll
-  for (int e = 0; e < E; ++e) {
-    x[e] = (double)raw[e];
-    nan |= (x[e] != x[e]);
-  }
-  double s;
-  if constexpr (E < 8) {
-    s = x[0];
-#pragma unroll
-    for (int e = 1; e < E; ++e) s += x[e];
-  } else {
-    s = np_sum<E>(x);
-  }
-  const double mean = div_small_int(s, dE, invE);
-  double d[E];
-#pragma unroll
-  for (int e = 0; e < E; ++e) {
-    const double t = x[e] - mean;
-    d[e] = t * t;
-  }
-  double ss;
-  if constexpr (E < 8) {
-    ss = d[0];
-#pragma unroll
-    for (int e = 1; e < E; ++e) ss += d[e];
-  } else {
-    ss = np_sum<E>(d);
-  }
-  var = div_small_int(div_small_int(ss, dE, invE), dE, invE);
-  if (median)
-    median_of<E, T>(raw, avg);
-  else
-    avg = mean;
-  if (nan) {
-    avg = __builtin_nan("");
-    var = __builtin_nan("");
-  }
+  ensemble_reduce<E, T>(raw, median, avg, var);
 }
 
 // ---------------------------------------------------------------------------

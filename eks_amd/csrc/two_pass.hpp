@@ -606,7 +606,9 @@ __global__ __launch_bounds__(64 * kWV) void k3_bwd(SmoothArgs a, Plan3 p) {
     const bool live = lane_ok && f < p.NCf;
     bool ok = true, okc = true;  // recursions, and the chain wait
     Model<R, N> md;
-    double Mr[NR][KS];  // filtered states of the last NR steps
+    // the last NR steps keep their RTS gains (J_t, d_t) from the forward
+    // sweep in registers; the first NL keep filtered states in LDS
+    double Jr[NR][R][R], dr[NR][R];
     Affine<R> Mp;       // this chunk's RTS map: ms[s] = G ms[e] + g
     Mp.set_identity();
     const long long s = f * p.L, e = min(TT, s + p.L);
@@ -644,8 +646,8 @@ __global__ __launch_bounds__(64 * kWV) void k3_bwd(SmoothArgs a, Plan3 p) {
           for (int j = 0; j < N; ++j) y[j] = avg[j] - md.off[j];
           if (tt > 0) kf_predict<R, AI>(m, P, md.A, md.Q);
           kf_update<R, N, CI, decltype(acc)>(m, P, md.C, y, rv, acc, ok);
-          double st[KS];
-          {
+          if (i < NL) {
+            double st[KS];
             int k = 0;
 #pragma unroll
             for (int u = 0; u < R; ++u) st[k++] = m[u];
@@ -653,19 +655,23 @@ __global__ __launch_bounds__(64 * kWV) void k3_bwd(SmoothArgs a, Plan3 p) {
             for (int u = 0; u < R; ++u)
 #pragma unroll
               for (int v = u; v < R; ++v) st[k++] = P[u][v];
-          }
-          if (i < NL) {
 #pragma unroll
             for (int u = 0; u < KS; ++u) fs[i < NL ? i : 0][u][tid] = st[u];
-          } else {
-#pragma unroll
-            for (int u = 0; u < KS; ++u) Mr[i >= NL ? i - NL : 0][u] = st[u];
           }
+          const int ir = i >= NL ? i - NL : 0;
           // the chunk's map in forward order: G <- G J_t, g <- g + G d_t
           // (the trajectory's last step: ms[T-1] = mf[T-1], a constant)
           if (tt + 1 < TT) {
             double J[R][R], d[R];
             ok = rts_gain<R, AI>(m, P, md.A, md.Q, J, d) && ok;
+            if (i >= NL) {
+#pragma unroll
+              for (int u = 0; u < R; ++u) {
+                dr[ir][u] = d[u];
+#pragma unroll
+                for (int v = 0; v < R; ++v) Jr[ir][u][v] = J[u][v];
+              }
+            }
             Affine<R> step;
 #pragma unroll
             for (int u = 0; u < R; ++u) {
@@ -675,6 +681,10 @@ __global__ __launch_bounds__(64 * kWV) void k3_bwd(SmoothArgs a, Plan3 p) {
             }
             Mp = Mp.after(step);
           } else {
+            if (i >= NL) {
+#pragma unroll
+              for (int u = 0; u < R; ++u) dr[ir][u] = m[u];
+            }
 #pragma unroll
             for (int u = 0; u < R; ++u) {
               double sg = Mp.g[u];
@@ -823,7 +833,17 @@ __global__ __launch_bounds__(64 * kWV) void k3_bwd(SmoothArgs a, Plan3 p) {
       for (int i = LF - 1; i >= NL; --i) {
         const long long tt = s + i;
         if (tt < e) {
-          rts_step(Mr[i - NL], tt);
+          double nx[R];
+#pragma unroll
+          for (int u = 0; u < R; ++u) {
+            double sm = dr[i - NL][u];
+#pragma unroll
+            for (int v = 0; v < R; ++v) sm = fma(Jr[i - NL][u][v], ms[v], sm);
+            nx[u] = sm;
+          }
+          const bool last = tt + 1 == TT;  // ms[T-1] = mf[T-1] (J_t unset)
+#pragma unroll
+          for (int u = 0; u < R; ++u) ms[u] = last ? dr[i - NL][u] : nx[u];
           emit(tt);
         }
       }
