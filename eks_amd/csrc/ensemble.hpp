@@ -17,6 +17,15 @@ namespace eks {
 template <typename T>
 EKS_DEV double to_f64(T v) { return static_cast<double>(v); }
 
+// A rounded product the compiler may not fuse into its consumers (x - mean,
+// P + var, ...): with fp-contract the fusion would depend on where the
+// function is inlined, and a kernel reading y / ev from the fit's planes must
+// see the same bits as one computing them itself.
+EKS_DEV double rounded(double v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
 // numpy-order summation of a register array: numpy's pairwise_sum rule for
 // n <= 128 (sequential below 8 elements, 8 interleaved partial sums above).
 template <int E>
@@ -106,14 +115,14 @@ EKS_DEV void ensemble_reduce(const T (&raw)[E], bool median, double &avg, double
     x[e] = to_f64(raw[e]);
     has_nan |= (raw[e] != raw[e]);
   }
-  const double mean = np_sum<E>(x) * invE;
+  const double mean = rounded(np_sum<E>(x) * invE);
   double d[E];
 #pragma unroll
   for (int e = 0; e < E; ++e) {
     const double t = x[e] - mean;
     d[e] = t * t;
   }
-  var = np_sum<E>(d) * invE2;  // NaN members make it NaN by themselves
+  var = rounded(np_sum<E>(d) * invE2);  // NaN members make it NaN by themselves
   if (median) {
     avg = median_of<E, T>(raw);
     if (has_nan) avg = __builtin_nan("");  // the selection would skip them
@@ -149,11 +158,11 @@ EKS_DEV void ensemble_reduce_rt(const T *p, long long se, int E, bool median, do
   };
   // the compiled path's arithmetic (products by the reciprocals)
   const double invE = 1.0 / (double)E, invE2 = 1.0 / ((double)E * (double)E);
-  const double mean = np_sum_rt([&](int i) { return to_f64(p[(long long)i * se]); }) * invE;
-  var = np_sum_rt([&](int i) {
+  const double mean = rounded(np_sum_rt([&](int i) { return to_f64(p[(long long)i * se]); }) * invE);
+  var = rounded(np_sum_rt([&](int i) {
           const double t = to_f64(p[(long long)i * se]) - mean;
           return t * t;
-        }) * invE2;
+        }) * invE2);
   for (int e = 0; e < E; ++e) {
     const double v = to_f64(p[(long long)e * se]);
     has_nan |= (v != v);

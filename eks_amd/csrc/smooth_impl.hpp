@@ -41,6 +41,7 @@
 #include "../../include/eks_hip.h"
 #include "eks_common.hpp"
 #include "ensemble.hpp"
+#include "handoff.hpp"
 #include "kf_steps.hpp"
 #include "small_linalg.hpp"
 
@@ -141,13 +142,14 @@ inline bool uniform_lanes(long long B);
 // Many trajectories (whole blocks per chunk): short enough that B * NC lanes
 // fill the GPU (L_fill), long enough that the chunk scans stay short
 // (L_scan = sqrt(2 T / 64)).
-// Few trajectories (chunk-major lanes): the chip cannot be filled anyway, so
-// L balances the per-lane serial chunk work (~ L steps) against the serial
-// part of the block-parallel chunk scans (~ 2 NC / 512 element compositions):
-// L = sqrt(2 T rho / 512), rho = composition / step cost ratio, measured 2.6
-// for r <= 2 and 0.8 for r = 3 (configs 2, 3, 5: EKS_CHUNK_LEN sweeps; config
-// 5 with the pupil kernels and the prefetched K2: L = 40 / 56 / 72 / 96 ->
-// 3.41 / 3.20 / 3.33 / ~3.5 ms per step, tools/c5_sweep.sh).
+// Few trajectories (chunk-major lanes): the per-step FP64 work of K1 / K3 /
+// K5 keeps a SIMD busy with one wave (a second wave per SIMD buys ~nothing:
+// config 2 at L = 16 vs 32), so L is as long as still gives every SIMD a
+// wave: L_fill = B T / (1024 SIMDs x 64 lanes), at least kMinChunk; and at
+// most the length that balances the per-lane chunk work against the chunk
+// scans' compositions, L_scan = sqrt(2 T rho / 512), rho = composition /
+// step cost ratio (2.6 for r <= 2, 0.8 for r = 3).  Config 5's B = 1 smooth
+// of 1M frames: L 56 -> 16, its K3 + K5 0.49 -> 0.20 ms.
 inline long long chunk_len(long long B, long long T, int r) {
   const long long ls = 8;  // a multiple of every checkpoint interval
   static const long long forced = [] {  // EKS_CHUNK_LEN: tuning experiments only
@@ -163,7 +165,9 @@ inline long long chunk_len(long long B, long long T, int r) {
     L = std::max(kMinChunk, std::max(l_fill, l_scan));
   } else {
     const double rho = r <= 2 ? 2.6 : 0.8;
-    L = std::max(kMinChunk, (long long)std::llround(std::sqrt(2.0 * (double)T * rho / 512.0)));
+    const long long l_scan = std::llround(std::sqrt(2.0 * (double)T * rho / 512.0));
+    const long long l_fill = (B * T + 65535) / 65536;
+    L = std::max(kMinChunk, std::min(l_fill, l_scan));
   }
   L = round_up(L, ls);
   if (L >= T) L = round_up(T, ls);
@@ -187,6 +191,17 @@ struct ChunkPlan {
   EKS_DEV unsigned ylane(unsigned b) const { return yB == 1 ? 0u : b; }
   size_t y_off = 0, ev_off = 0, elem_off = 0, cstart_off = 0, bwd_off = 0, nllp_off = 0,
          msend_off = 0, ckpt_off = 0, total = 0;
+  // chained chunk scans (k_c2_fscan_g / k_c4_bscan_g): G blocks per
+  // trajectory, block g owning chunks [g CPB, (g+1) CPB); their sync words
+  // (two tickets, then per-(trajectory, block) flags: K2 totals, K2 NLL
+  // partials, K4 totals) are zeroed by K1 (or a memset) every call
+  int G = 1;
+  long long CPB = 0;
+  size_t sync_off = 0, sync_bytes = 0, agg_off = 0, magg_off = 0, part_off = 0;
+  EKS_DEV unsigned *sync(char *ws) const { return (unsigned *)(ws + sync_off); }
+  EKS_DEV unsigned *flags(char *ws, int k, long long B) const {
+    return sync(ws) + 64 + (size_t)k * (size_t)B * (size_t)G;
+  }
   // where K3 / K5 read y / ev: the workspace planes K1 wrote, or (EKS_YEV
   // input) the caller's planes
   const char *ysrc = nullptr, *evsrc = nullptr;
@@ -215,6 +230,22 @@ inline ChunkPlan make_plan(long long B, long long T, int r, int n, long long L) 
   p.nllp_off = take((size_t)p.NC * Bz * 8);
   p.msend_off = take((size_t)p.NC * r * Bz * 8);
   p.ckpt_off = take((size_t)p.NC * p.NSUB * state_len(r) * Bz * 8);
+  if (p.NC > wave_scan_chunks()) {
+    // blocks per trajectory: few lanes in all -> ~1 chunk per thread (the
+    // scan is latency bound); many -> q chunks per thread so the chip holds
+    // ~4 blocks per CU (the Hillis-Steele trees cost ~6 compositions per
+    // lane, the per-thread runs 1 per chunk: config 5's 64 x 17 858 chunks).
+    // At most 64 blocks: their totals are combined by one wave.
+    const long long qt = std::min<long long>(8, std::max<long long>(1, B * p.NC / (256LL * 256 * 4)));
+    p.G = (int)std::min<long long>(64, std::max<long long>(1, (p.NC + 256 * qt - 1) / (256 * qt)));
+    p.CPB = (p.NC + p.G - 1) / p.G;
+    const size_t BG = Bz * (size_t)p.G;
+    p.sync_bytes = align256(256 + 3 * BG * 4);
+    p.sync_off = take(p.sync_bytes);
+    p.agg_off = take(BG * elem_len(r) * 8);
+    p.magg_off = take(BG * (r * r + r) * 8);
+    p.part_off = take(BG * 2 * 8);
+  }
   p.total = off;
   return p;
 }
@@ -721,8 +752,17 @@ EKS_DEV void c1_chunk(const SmoothArgs &a, const ChunkPlan &p, long long c, unsi
   if (!ok) flag(a.status, b, first ? EKS_STATUS_SINGULAR : EKS_STATUS_SCAN);
 }
 
+// zero the chained scans' sync words for K2 / K4 of this call (block 0 of K1:
+// stream order makes them visible to the scans without a memset launch)
+EKS_DEV void zero_scan_sync(const SmoothArgs &a, const ChunkPlan &p) {
+  if (blockIdx.x != 0 || p.sync_bytes == 0) return;
+  unsigned *z = p.sync(a.ws);
+  for (size_t i = threadIdx.x; i < p.sync_bytes / 4; i += blockDim.x) z[i] = 0u;
+}
+
 template <int R, int N, int E, typename T, typename YT, int AI, int CI, bool UNI>
 EKS_DEV void c1_elem_body(const SmoothArgs &a, const ChunkPlan &p) {
+  zero_scan_sync(a, p);
   Lane<UNI> ln;
   if (!ln.init(a.B, p.NC)) return;
   c1_chunk<R, N, E, T, YT, AI, CI, UNI>(a, p, ln.c, ln.b);
@@ -815,90 +855,169 @@ EKS_DEV void elem_run(const double *rows, long long c0, long long c1, F &&fn) {
   }
 }
 
-// K2, parallel form: one block of W waves per trajectory for many chunks.
-// Thread l owns chunks [l q, (l+1) q): it composes their elements, each wave
-// scans its 64 aggregates (Hillis-Steele, log2 64 = 6 compositions), the
-// wave totals are combined through LDS (W - 1 compositions at most), and each
-// thread then walks its chunks from its exclusive prefix.  Latency
-// O(q + 6 + W + q) element compositions instead of O(NC).
-template <int R, int N, int W>
-__global__ __launch_bounds__(64 * W) void k_c2_fscan_w(SmoothArgs a, ChunkPlan p) {
-  __shared__ double tot[W][Elem<R>::len];
-  const long long b = blockIdx.x;
-  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+// whole elements through the hand-off primitives (handoff.hpp)
+template <int R>
+EKS_DEV void elem_store_wt(const Elem<R> &E, double *p) {
+  double v[Elem<R>::len];
+  E.store(v, 1);
+#pragma unroll
+  for (int k = 0; k < Elem<R>::len; ++k) st_wt(p + k, v[k]);
+}
+template <int R>
+EKS_DEV void elem_load_wt(Elem<R> &E, const double *p) {
+  double v[Elem<R>::len];
+#pragma unroll
+  for (int k = 0; k < Elem<R>::len; ++k) v[k] = ld_wt(p + k);
+  E.load(v, 1);
+}
+
+// K2, chained form (many chunks per trajectory): G blocks of 4 waves per
+// trajectory, taken from a ticket counter so that the blocks of trajectory
+// b hold consecutive tickets and a block only ever waits for blocks with
+// smaller tickets (already running or done: every wait ends).
+//  1. thread tid of block g owns chunks [c0, c1) (q = CPB / 256, ~1): it
+//     composes their elements; each wave scans its 64 aggregates
+//     (Hillis-Steele, 6 compositions); the wave totals are combined in LDS;
+//     the block total is published (write-through stores + flag);
+//  2. wave 0 gathers the totals of blocks 0..g-1 (one per lane) and scans
+//     them with the same Hillis-Steele tree: lane g-1 holds the block's
+//     exclusive prefix;
+//  3. each thread walks its chunks from its exclusive prefix, writing the
+//     chunk start states (and, filter-only calls, the closed-form NLL
+//     shares; fused: per-block sums, added in block order by block G-1).
+// The association order of every composition depends on (NC, G) alone, so
+// results are deterministic.  Latency: ~2q + 6 + 3 + 6 compositions and two
+// hand-offs whatever NC (the single-block form was ~2 NC / 256 chunk loads
+// in sequence: config 2's K2 31.8 us).
+template <int R, int N>
+__global__ __launch_bounds__(256) void k_c2_fscan_g(SmoothArgs a, ChunkPlan p) {
+  constexpr int W = 4, EL = Elem<R>::len, KS = R + Sym<R>::len;
+  __shared__ double tot[W][EL];
+  __shared__ double bpre[EL];
+  __shared__ double ns[W];
+  __shared__ unsigned tk;
+  const int tid = threadIdx.x, l = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  unsigned *sync = p.sync(a.ws);
+  if (tid == 0) tk = atomicAdd(sync, 1u);
+  __syncthreads();
   const long long B = a.B, NC = p.NC;
+  const int G = p.G;
+  const unsigned t = __builtin_amdgcn_readfirstlane(tk);
+  const long long b = t / (unsigned)G;
+  const int g = (int)(t - (unsigned)b * (unsigned)G);
   if (b >= B) return;
-  constexpr int KS = R + Sym<R>::len;
   const double *elem = (const double *)(a.ws + p.elem_off);
+  const double *erow = elem + b * NC * EL;
   double *cst = (double *)(a.ws + p.cstart_off);
-  const long long q = (NC + 64 * W - 1) / (64 * W);
-  const long long c0 = min(NC, (long long)tid * q), c1 = min(NC, c0 + q);
+  unsigned *fl_tot = p.flags(a.ws, 0, B) + b * G, *fl_nll = p.flags(a.ws, 1, B) + b * G;
+  double *aggs = (double *)(a.ws + p.agg_off) + b * G * EL;
+  double *parts = (double *)(a.ws + p.part_off) + b * G;
+  const long long cb0 = (long long)g * p.CPB, cb1 = min(NC, cb0 + p.CPB);
+  const long long q = (p.CPB + 255) / 256;
+  const long long c0 = min(cb1, cb0 + tid * q), c1 = min(cb1, c0 + q);
   bool ok = true;
   Elem<R> agg;
   agg.set_identity();
-  elem_run<R>(elem + b * NC * Elem<R>::len, c0, c1, [&](long long, const Elem<R> &e) {
-    Elem<R> t;
-    ok = compose_elem<R>(agg, e, t) && ok;
-    agg = t;
+  elem_run<R>(erow, c0, c1, [&](long long c, const Elem<R> &e) {
+    if (c == c0) {
+      agg = e;
+    } else {
+      Elem<R> tt;
+      ok = compose_elem<R>(agg, e, tt) && ok;
+      agg = tt;
+    }
   });
 #pragma unroll
   for (int k = 1; k < 64; k <<= 1) {
     const Elem<R> o = shfl_elem<R, true>(agg, k);
     if (l >= k) {
-      Elem<R> t;
-      ok = compose_elem<R>(o, agg, t) && ok;
-      agg = t;
+      Elem<R> tt;
+      ok = compose_elem<R>(o, agg, tt) && ok;
+      agg = tt;
     }
   }
   Elem<R> ex = shfl_elem<R, true>(agg, 1);
-  if constexpr (W > 1) {
-    if (l == 0) ex.set_identity();
-    if (l == 63) agg.store(tot[w], 1);
-    __syncthreads();
-    if (w > 0) {  // prefix of the earlier waves' totals, in order
-      Elem<R> pre;
-      pre.load(tot[0], 1);
-      for (int v = 1; v < w; ++v) {
-        Elem<R> tv, t;
-        tv.load(tot[v], 1);
-        ok = compose_elem<R>(pre, tv, t) && ok;
-        pre = t;
-      }
-      if (l == 0) {
-        ex = pre;
-      } else {
-        Elem<R> t;
-        ok = compose_elem<R>(pre, ex, t) && ok;
-        ex = t;
-      }
+  if (l == 0) ex.set_identity();
+  if (l == 63) agg.store(tot[w], 1);
+  __syncthreads();
+  Elem<R> pre;  // the totals of the block's earlier waves, in order
+  if (w > 0) {
+    pre.load(tot[0], 1);
+    for (int v = 1; v < w; ++v) {
+      Elem<R> tv, tt;
+      tv.load(tot[v], 1);
+      ok = compose_elem<R>(pre, tv, tt) && ok;
+      pre = tt;
+    }
+    if (l == 0) {
+      ex = pre;
+    } else {
+      Elem<R> tt;
+      ok = compose_elem<R>(pre, ex, tt) && ok;
+      ex = tt;
     }
   }
+  if (w == W - 1 && g + 1 < G) {  // the block total, for the later blocks
+    Elem<R> tv, bt;
+    tv.load(tot[W - 1], 1);
+    ok = compose_elem<R>(pre, tv, bt) && ok;
+    if (l == 0) elem_store_wt<R>(bt, aggs + (long long)g * EL);
+    publish_flag(fl_tot + g, l);
+  }
+  if (g > 0) {  // the totals of blocks 0..g-1
+    if (w == 0) {
+      Elem<R> e;
+      e.set_identity();
+      if (!wait_flag_lanes(fl_tot + l, l < g)) ok = false;
+      if (l < g) elem_load_wt<R>(e, aggs + (long long)l * EL);
+      for (int k = 1; k < g; k <<= 1) {  // levels past g - 1 leave lanes < g alone
+        const Elem<R> o = shfl_elem<R, true>(e, k);
+        if (l >= k) {
+          Elem<R> tt;
+          ok = compose_elem<R>(o, e, tt) && ok;
+          e = tt;
+        }
+      }
+      if (l == g - 1) e.store(bpre, 1);
+    }
+    __syncthreads();
+    Elem<R> bp;
+    bp.load(bpre, 1);
+    if (tid == 0) {
+      ex = bp;
+    } else {
+      Elem<R> tt;
+      ok = compose_elem<R>(bp, ex, tt) && ok;
+      ex = tt;
+    }
+  }
+  const bool first = g == 0 && tid == 0;  // owns chunk 0
   double nsum = 0.0;  // this thread's NLL shares (nll_fused)
   if (c0 < c1 && a.t_base > 0) {
     // a later time segment: every thread starts from the handed-over state
     // composed with the elements before its first chunk
     double m[R], P[R][R];
-    load_state<R>(a.seg_in + b * (R + Sym<R>::len), 1, m, P);
-    if (tid > 0) ok = compose_state<R>(m, P, ex) && ok;
+    load_state<R>(a.seg_in + b * KS, 1, m, P);
+    if (!first) ok = compose_state<R>(m, P, ex) && ok;
     for (long long c = c0; c < c1; ++c) {
       store_state<R>(cst + (c * KS) * B + b, B, m, P);
       if (c + 1 < c1) {
         Elem<R> e;
-        e.load(elem + (b * NC + c) * Elem<R>::len, 1);
+        e.load(erow + c * EL, 1);
         ok = compose_state<R>(m, P, e) && ok;
       }
     }
   } else if (c0 < c1) {
     double m[R], P[R][R];
     long long c = c0;
-    if (tid == 0) {
+    if (first) {
       using L = ParamLayout<R, N>;
       const double *pp = a.params + b * L::len;
       load_vec<R>(pp + L::m0, m);
       load_mat<R, R>(pp + L::S0, P);
       store_state<R>(cst + b, B, m, P);  // chunk 0 starts from the prior
       Elem<R> e0;
-      e0.load(elem + b * NC * Elem<R>::len, 1);
+      e0.load(erow, 1);
 #pragma unroll
       for (int i = 0; i < R; ++i) {
         m[i] = e0.bb[i];
@@ -907,6 +1026,8 @@ __global__ __launch_bounds__(64 * W) void k_c2_fscan_w(SmoothArgs a, ChunkPlan p
       }
       c = 1;
     } else {
+      // chunk 0's element is the filtered state itself (Ab = 0), so the
+      // prefix is the state entering c0
 #pragma unroll
       for (int i = 0; i < R; ++i) {
         m[i] = ex.bb[i];
@@ -916,7 +1037,7 @@ __global__ __launch_bounds__(64 * W) void k_c2_fscan_w(SmoothArgs a, ChunkPlan p
     }
     double *np_ = (double *)(a.ws + p.nllp_off);
     const bool need = !p.nll_closed;  // the start states feed K3 / K5 (not a closed-form NLL call)
-    elem_run<R>(elem + b * NC * Elem<R>::len, c, c1, [&](long long c, const Elem<R> &e) {
+    elem_run<R>(erow, c, c1, [&](long long c, const Elem<R> &e) {
       if (need) store_state<R>(cst + (c * KS) * B + b, B, m, P);
       if (p.nll_closed) {
         const double sh = elem_nll_share<R>(m, P, e, np_[c * B + b], ok);
@@ -925,18 +1046,29 @@ __global__ __launch_bounds__(64 * W) void k_c2_fscan_w(SmoothArgs a, ChunkPlan p
       }
       if (c + 1 < c1) ok = compose_state<R>(m, P, e) && ok;
     });
-    if (tid == 0 && p.nll_fused) nsum += np_[b];  // chunk 0's share: the plain filter's (K1)
+    if (first && p.nll_fused) nsum += np_[b];  // chunk 0's share: the plain filter's (K1)
   }
-  if (p.nll_fused) {  // the NLL sum: per thread in chunk order, then the block (fixed order)
+  if (p.nll_fused) {  // per thread in chunk order, the block (fixed order), then the blocks in order
 #pragma unroll
     for (int k = 32; k >= 1; k >>= 1) nsum += __shfl_xor(nsum, k, 64);
-    __shared__ double ns[W];
     if (l == 0) ns[w] = nsum;
     __syncthreads();
-    if (tid == 0) {
-      double t = ns[0];
-      for (int v = 1; v < W; ++v) t += ns[v];
-      a.nll[b] = t;
+    double s = ns[0];
+    for (int v = 1; v < W; ++v) s += ns[v];
+    if (G == 1) {
+      if (tid == 0) a.nll[b] = s;
+    } else if (w == 0) {
+      if (g + 1 < G) {
+        if (l == 0) st_wt(parts + g, s);
+        publish_flag(fl_nll + g, l);
+      } else {  // the last block adds the partial sums in block order
+        if (!wait_flag_lanes(fl_nll + l, l < g)) ok = false;
+        if (l == 0) {
+          double tsum = 0.0;
+          for (int v = 0; v < g; ++v) tsum += ld_wt(parts + v);
+          a.nll[b] = tsum + s;
+        }
+      }
     }
   }
   if (!ok) flag(a.status, b, EKS_STATUS_SCAN);
@@ -978,22 +1110,59 @@ struct Affine {
   }
 };
 
-// K4, parallel form: chunk maps ms_start[c] = G_c ms_start[c+1] + g_c
-// composed right-to-left per thread, a suffix scan over the lanes of each
-// wave, the wave totals combined through LDS, then each thread walks its
-// chunks; NLL shares summed by a block reduction (fixed order).
-template <int R, int W>
-__global__ __launch_bounds__(64 * W) void k_c4_bscan_w(SmoothArgs a, ChunkPlan p) {
-  __shared__ double tot[W][R * R + R];
+template <int R>
+EKS_DEV void map_store_wt(const Affine<R> &F, double *p) {
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    st_wt(p + R * R + i, F.g[i]);
+#pragma unroll
+    for (int j = 0; j < R; ++j) st_wt(p + i * R + j, F.G[i][j]);
+  }
+}
+template <int R>
+EKS_DEV void map_load_wt(Affine<R> &F, const double *p) {
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    F.g[i] = ld_wt(p + R * R + i);
+#pragma unroll
+    for (int j = 0; j < R; ++j) F.G[i][j] = ld_wt(p + i * R + j);
+  }
+}
+
+// K4, chained form: chunk maps ms_start[c] = G_c ms_start[c+1] + g_c, G
+// blocks of 4 waves per trajectory as in K2 but in reverse: the tickets of
+// trajectory b go to its blocks g = G-1 .. 0, and a block waits only for the
+// later blocks' totals.  Each thread composes its chunks' maps right to
+// left, each wave suffix-scans its lanes, the wave totals are combined in
+// LDS, the block total (and the block's NLL partial sum) is published; wave
+// 0 then suffix-scans the totals of blocks g+1..G-1 and each thread walks
+// its chunks from the smoothed mean entering its last one.  Block 0, which
+// waits for every other block, adds the NLL partial sums in block order.
+template <int R>
+__global__ __launch_bounds__(256) void k_c4_bscan_g(SmoothArgs a, ChunkPlan p) {
+  constexpr int W = 4, MR = R * R + R;
+  __shared__ double tot[W][MR];
+  __shared__ double bsuf[MR];
   __shared__ double nsum[W];
-  const long long b = blockIdx.x;
-  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+  __shared__ unsigned tk;
+  const int tid = threadIdx.x, l = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  unsigned *sync = p.sync(a.ws);
+  if (tid == 0) tk = atomicAdd(sync + 32, 1u);
+  __syncthreads();
   const long long B = a.B, NC = p.NC;
+  const int G = p.G;
+  const unsigned t = __builtin_amdgcn_readfirstlane(tk);
+  const long long b = t / (unsigned)G;
+  const int g = G - 1 - (int)(t - (unsigned)b * (unsigned)G);
   if (b >= B) return;
   const double *bw = (const double *)(a.ws + p.bwd_off);
   double *msend = (double *)(a.ws + p.msend_off);
-  const long long q = (NC + 64 * W - 1) / (64 * W);
-  const long long c0 = min(NC, (long long)tid * q), c1 = min(NC, c0 + q);
+  unsigned *fl = p.flags(a.ws, 2, B) + b * G;
+  double *maggs = (double *)(a.ws + p.magg_off) + b * G * MR;
+  double *parts = (double *)(a.ws + p.part_off) + B * G + b * G;
+  const long long cb0 = (long long)g * p.CPB, cb1 = min(NC, cb0 + p.CPB);
+  const long long q = (p.CPB + 255) / 256;
+  const long long c0 = min(cb1, cb0 + tid * q), c1 = min(cb1, c0 + q);
   auto load_map = [&](const double *s) {
     Affine<R> f;
 #pragma unroll
@@ -1004,7 +1173,7 @@ __global__ __launch_bounds__(64 * W) void k_c4_bscan_w(SmoothArgs a, ChunkPlan p
     }
     return f;
   };
-  auto map_of = [&](long long c) { return load_map(bw + (b * NC + c) * (R * R + R)); };
+  auto map_of = [&](long long c) { return load_map(bw + (b * NC + c) * MR); };
   // fn(c, map c) for c = c1-1 down to c0, PD maps in flight (see elem_run)
   auto map_run = [&](auto &&fn) {
     constexpr int PD = 2 * scan_pd<R>();
@@ -1031,22 +1200,72 @@ __global__ __launch_bounds__(64 * W) void k_c4_bscan_w(SmoothArgs a, ChunkPlan p
   }
   Affine<R> X = F.shfl_down(1);
   if (l == 63) X.set_identity();
-  if constexpr (W > 1) {
+  double s = 0.0;  // NLL shares of this thread's chunks, then of the wave
+  if (a.nll) {
+    const double *np_ = (const double *)(a.ws + p.nllp_off);
+    for (long long c = c0; c < c1; ++c) s += np_[c * B + b];
+#pragma unroll
+    for (int k = 32; k >= 1; k >>= 1) s += __shfl_xor(s, k, 64);
+  }
+  if (l == 0) {
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      tot[w][R * R + i] = F.g[i];
+#pragma unroll
+      for (int j = 0; j < R; ++j) tot[w][i * R + j] = F.G[i][j];
+    }
+    nsum[w] = s;
+  }
+  __syncthreads();
+  Affine<R> S;  // the later waves' totals
+  S.set_identity();
+  if (w + 1 < W) {
+    S = load_map(tot[W - 1]);
+    for (int v = W - 2; v > w; --v) S = load_map(tot[v]).after(S);
+    X = X.after(S);
+  }
+  double part = nsum[0];  // the block's NLL partial, waves in order
+  for (int v = 1; v < W; ++v) part += nsum[v];
+  bool ok = true;
+  if (w == 0 && g > 0) {  // the block total (and partial), for the earlier blocks
+    const Affine<R> T0 = load_map(tot[0]).after(S);
     if (l == 0) {
+      map_store_wt<R>(T0, maggs + (long long)g * MR);
+      st_wt(parts + g, part);
+    }
+    publish_flag(fl + g, l);
+  }
+  if (g + 1 < G) {  // the totals of blocks g+1..G-1
+    if (w == 0) {
+      Affine<R> e;
+      e.set_identity();
+      const bool need = l > g && l < G;
+      if (!wait_flag_lanes(fl + l, need)) ok = false;
+      if (need) map_load_wt<R>(e, maggs + (long long)l * MR);
+      for (int k = 1; k < G - 1 - g; k <<= 1) {  // lane g+1 needs G-1-g lanes
+        const Affine<R> o = e.shfl_down(k);
+        if (l + k < 64) e = e.after(o);
+      }
+      if (l == g + 1) {
 #pragma unroll
-      for (int i = 0; i < R; ++i) {
-        tot[w][R * R + i] = F.g[i];
+        for (int i = 0; i < R; ++i) {
+          bsuf[R * R + i] = e.g[i];
 #pragma unroll
-        for (int j = 0; j < R; ++j) tot[w][i * R + j] = F.G[i][j];
+          for (int j = 0; j < R; ++j) bsuf[i * R + j] = e.G[i][j];
+        }
+      }
+      if (a.nll && g == 0 && l == 0) {  // every other block's partial is visible now
+        double tsum = part;
+        for (int v = 1; v < G; ++v) tsum += ld_wt(parts + v);
+        a.nll[b] = tsum;
       }
     }
     __syncthreads();
-    if (w + 1 < W) {  // suffix of the later waves' totals
-      Affine<R> S = load_map(tot[W - 1]);
-      for (int v = W - 2; v > w; --v) S = load_map(tot[v]).after(S);
-      X = X.after(S);
-    }
+    X = X.after(load_map(bsuf));
+  } else if (a.nll && G == 1 && tid == 0) {
+    a.nll[b] = part;
   }
+  if (!ok) flag(a.status, b, EKS_STATUS_SCAN);
   double ms[R];
   // X maps the value entering the last chunk (none for the globally last
   // segment: its map is constant; the next segment's ms otherwise)
@@ -1074,24 +1293,6 @@ __global__ __launch_bounds__(64 * W) void k_c4_bscan_w(SmoothArgs a, ChunkPlan p
 #pragma unroll
     for (int i = 0; i < R; ++i) ms[i] = nx[i];
   });
-  if (a.nll) {
-    const double *np_ = (const double *)(a.ws + p.nllp_off);
-    double s = 0.0;
-    for (long long c = c0; c < c1; ++c) s += np_[c * B + b];
-#pragma unroll
-    for (int k = 32; k >= 1; k >>= 1) s += __shfl_xor(s, k, 64);
-    if constexpr (W > 1) {
-      if (l == 0) nsum[w] = s;
-      __syncthreads();
-      if (tid == 0) {
-        double t = nsum[0];
-        for (int v = 1; v < W; ++v) t += nsum[v];
-        a.nll[b] = t;
-      }
-    } else {
-      if (l == 0) a.nll[b] = s;
-    }
-  }
 }
 
 // Time-sharded smoothing (eks_smooth_seg): the aggregate of a segment's
@@ -1622,19 +1823,20 @@ int launch_shape(const SmoothArgs &a, int algo, long long L) {
     // wave per trajectory (log-depth scan) when it is long
     const bool wave_scan = p.NC > wave_scan_chunks();
     const int sw = scan_waves(p.NC);
+    const unsigned gscan = (unsigned)(a.B * p.G);  // k_c2_fscan_g / k_c4_bscan_g blocks
+    // the chained scans' sync words: zeroed by K1 in a whole-pipeline call
+    auto zero_sync = [&]() -> int {
+      if (hipMemsetAsync(a.ws + p.sync_off, 0, p.sync_bytes, a.stream) != hipSuccess)
+        return set_err(EKS_ERR_HIP, "eks_smooth: hipMemsetAsync failed");
+      return 0;
+    };
     if (ph == 0 || ph == 2) {
+      if (ph == 2 && wave_scan && (rc = zero_sync())) return rc;
       prof_mark(a.stream, "k_c2_fscan");
       if (!wave_scan)
         hipLaunchKernelGGL((k_c2_fscan<R, N>), dim3(g64), dim3(64), 0, a.stream, a, p);
-      else if (sw == 8)
-        hipLaunchKernelGGL((k_c2_fscan_w<R, N, 8>), dim3((unsigned)a.B), dim3(512), 0,
-                           a.stream, a, p);
-      else if (sw == 4)
-        hipLaunchKernelGGL((k_c2_fscan_w<R, N, 4>), dim3((unsigned)a.B), dim3(256), 0,
-                           a.stream, a, p);
       else
-        hipLaunchKernelGGL((k_c2_fscan_w<R, N, 1>), dim3((unsigned)a.B), dim3(64), 0, a.stream,
-                           a, p);
+        hipLaunchKernelGGL((k_c2_fscan_g<R, N>), dim3(gscan), dim3(256), 0, a.stream, a, p);
       if ((rc = check_launch("k_c2_fscan"))) return rc;
       if (p.nll_fused) {  // K2 summed the closed-form NLL shares: done
         prof_call_end(a.stream);
@@ -1667,15 +1869,12 @@ int launch_shape(const SmoothArgs &a, int algo, long long L) {
         return check_launch("k_c4_nll");
       }
     }
+    if (ph == 3 && wave_scan && (rc = zero_sync())) return rc;
     prof_mark(a.stream, "k_c4_bscan");
     if (!wave_scan)
       hipLaunchKernelGGL((k_c4_bscan<R>), dim3(g64), dim3(64), 0, a.stream, a, p);
-    else if (sw == 8)
-      hipLaunchKernelGGL((k_c4_bscan_w<R, 8>), dim3((unsigned)a.B), dim3(512), 0, a.stream, a, p);
-    else if (sw == 4)
-      hipLaunchKernelGGL((k_c4_bscan_w<R, 4>), dim3((unsigned)a.B), dim3(256), 0, a.stream, a, p);
     else
-      hipLaunchKernelGGL((k_c4_bscan_w<R, 1>), dim3((unsigned)a.B), dim3(64), 0, a.stream, a, p);
+      hipLaunchKernelGGL((k_c4_bscan_g<R>), dim3(gscan), dim3(256), 0, a.stream, a, p);
     if ((rc = check_launch("k_c4_bscan"))) return rc;
     prof_mark(a.stream, "k_c5_final");
     hipLaunchKernelGGL((k_c5_final<R, N, YT, AI, CI, LS, U>), dim3(gch), dim3(kBlock), 0,

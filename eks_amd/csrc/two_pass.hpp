@@ -114,41 +114,6 @@ inline Plan3 make_plan3(long long B, long long T, int r, int n) {
   return p;
 }
 
-// ---------------------------------------------------------------------------
-// in-launch hand-off primitives (agent scope, global address space)
-// ---------------------------------------------------------------------------
-typedef __attribute__((address_space(1))) unsigned k3_gu32;
-typedef __attribute__((address_space(1))) unsigned long long k3_gu64;
-
-EKS_DEV void st_wt(double *p, double v) {  // write-through (sc1) store
-  __hip_atomic_store((k3_gu64 *)p, __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
-}
-EKS_DEV double ld_wt(const double *p) {  // L1-bypassing (sc1) load
-  return __builtin_bit_cast(double, __hip_atomic_load((k3_gu64 *)p, __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_AGENT));
-}
-// publish: every payload store of this wave drained, then one flag store
-EKS_DEV void publish_flag(unsigned *flag, int lane) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (lane == 0) __hip_atomic_store((k3_gu32 *)flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// wait for a flag (the whole wave polls the one word); false on timeout
-// (~0.1 s: only a bug could get there, and then the call must still end)
-#ifndef EKS_K3_NOWAIT
-#define EKS_K3_NOWAIT 0  // 1: tuning experiment only -- skip the chain waits (wrong results)
-#endif
-EKS_DEV bool wait_flag(const unsigned *flag) {
-  if (EKS_K3_NOWAIT) return true;
-  unsigned spins = 0;
-  while (__hip_atomic_load((k3_gu32 *)flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
-    if (++spins > (1u << 16)) return false;
-    __builtin_amdgcn_s_sleep(2);
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the payload loads below the poll
-  return true;
-}
-
 // Step sources of the two member passes: a D-deep register ring of raw step
 // data, reduced to (raw average, variance) on use.
 // Raw buffer loads of the members: the step's base address goes into the

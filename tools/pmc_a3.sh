@@ -9,7 +9,7 @@ rm -f $OUT/summary.txt
 i=0
 for ctr in ${CTRS:-FETCH_SIZE WRITE_SIZE SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_BUSY_CYCLES GRBM_GUI_ACTIVE}; do
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --kernel-include-regex 'k3_' --pmc $ctr -d $RAW/p$i -o run --output-format csv -- \
+  timeout -s KILL 120 rocprofv3 --kernel-include-regex "${KRX:-k3_}" --pmc $ctr -d $RAW/p$i -o run --output-format csv -- \
       python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline ${BENCH_ARGS} > $OUT/p$i.log 2>&1 || exit $?
   f=$(find $RAW/p$i -name "*counter_collection.csv" | head -1)
   python3 - "$f" "$ctr" <<'PY' >> $OUT/summary.txt
