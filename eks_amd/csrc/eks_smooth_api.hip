@@ -62,7 +62,9 @@ size_t eks_smooth_workspace_bytes(int64_t B, int64_t T, int n, int r, int E, int
   if (use_rt(r, n, algo)) return seq_workspace_bytes(B, T, r);
   const int al = pick_algo(B, T, n, r, E, algo);
   if (al == 1) return seq_workspace_bytes(B, T, r);
-  const size_t p2 = make_plan(B, T, r, n, chunk_len(B, T, r)).total;
+  // smoothing calls of few trajectories use shorter chunks than filter-only ones
+  const size_t p2 = std::max(make_plan(B, T, r, n, chunk_len(B, T, r)).total,
+                             make_plan(B, T, r, n, chunk_len_smooth(B, T, r)).total);
   // algo 3 smooths only: a filter-only (NLL) call of the same shape runs algo 2
   return al == 3 ? std::max(p2, make_plan3(B, T, r, n).total) : p2;
 }
@@ -118,7 +120,7 @@ static int smooth_call(const void *obs, int obs_dtype, int64_t B, int64_t T, int
   a.seg_in = seg_in;
   a.seg_out = seg_out;
   if (rt) return launch_rt(a);  // model_flags are promises only: the general kernel serves all
-  long long L = chunk_len(B, T, r);
+  long long L = (out && phase == 0) ? chunk_len_smooth(B, T, r) : chunk_len(B, T, r);
   if (L >= T) L = (T + 7) / 8 * 8;
   if (r == 2 && n == 2) return launch_22(a, al, L);
   if (n == 4) return launch_34(a, al, L);

@@ -174,6 +174,18 @@ inline long long chunk_len(long long B, long long T, int r) {
   return L;
 }
 
+// Chunk length of a smoothing call: with few trajectories (B <= 256,
+// chunk-major lanes) the group-mode scans cost ~the same for any chunk
+// count, so the chunks are as short as the checkpoint grid allows
+// (kMinChunk): more waves per SIMD for K1 / K3 / K5 (config 2: L 32 -> 16,
+// 0.114 -> 0.104 ms per step).  Filter-only calls keep chunk_len's choice.
+inline long long chunk_len_smooth(long long B, long long T, int r) {
+  const long long L = chunk_len(B, T, r);
+  if (getenv("EKS_CHUNK_LEN") || uniform_lanes(B) || B > 256 || L >= T) return L;
+  const long long Ls = std::min(L, kMinChunk);
+  return (T + Ls - 1) / Ls > wave_scan_chunks() ? Ls : L;
+}
+
 struct ChunkPlan {
   long long L = 0, NC = 0, NSUB = 0;
   int LS = 8;
@@ -199,12 +211,34 @@ struct ChunkPlan {
   long long CPB = 0;
   size_t sync_off = 0, sync_bytes = 0, agg_off = 0, magg_off = 0, part_off = 0;
   EKS_DEV unsigned *sync(char *ws) const { return (unsigned *)(ws + sync_off); }
+  int GF = 1;  // the flag arrays' stride (max of the chunk- and group-level G)
   EKS_DEV unsigned *flags(char *ws, int k, long long B) const {
-    return sync(ws) + 64 + (size_t)k * (size_t)B * (size_t)G;
+    return sync(ws) + 64 + (size_t)k * (size_t)B * (size_t)GF;
   }
   // where K3 / K5 read y / ev: the workspace planes K1 wrote, or (EKS_YEV
   // input) the caller's planes
   const char *ysrc = nullptr, *evsrc = nullptr;
+  // Group mode (few trajectories, chunk-major lanes, smoothing calls): a
+  // *group* is the run of one trajectory's chunks inside one 256-lane block
+  // of K1 / K3 / K5 (B <= 256: every block holds ~256 / B consecutive chunks
+  // of every trajectory).  K1 scans its elements within the group (LDS) and
+  // stores inclusive prefixes plus the group total; K2 scans only the NG
+  // group totals per trajectory; K3 starts chunk c from its group's start
+  // state composed with the prefix before c, scans its RTS maps within the
+  // group right to left (suffixes, group totals, group NLL sums); K4 scans
+  // the group totals; K5 applies its suffix to the mean entering the group
+  // from the right.  The chained scans then see ~NC B / 256 groups instead
+  // of NC chunks per trajectory.
+  int grp = 0;
+  long long NG = 0;   // K1 blocks = groups per trajectory (the last may lack some b)
+  long long gnc = 0;  // in a K2 / K4 plan over groups: the chunk count (0 otherwise)
+  int GG = 1;         // G of the group-level scans
+  long long CPBG = 0;
+  size_t gagg_off = 0, gst_off = 0, gmap_off = 0, gms_off = 0, gnll_off = 0;
+  // groups of trajectory b in a plan over groups (the last block may not hold b)
+  EKS_DEV long long count_of(long long b, long long B) const {
+    return gnc ? ((gnc - 1) * B + b) / 256 + 1 : NC;
+  }
 };
 
 inline size_t align256(size_t x) { return (x + 255) / 256 * 256; }
@@ -236,10 +270,23 @@ inline ChunkPlan make_plan(long long B, long long T, int r, int n, long long L) 
     // ~4 blocks per CU (the Hillis-Steele trees cost ~6 compositions per
     // lane, the per-thread runs 1 per chunk: config 5's 64 x 17 858 chunks).
     // At most 64 blocks: their totals are combined by one wave.
-    const long long qt = std::min<long long>(8, std::max<long long>(1, B * p.NC / (256LL * 256 * 4)));
-    p.G = (int)std::min<long long>(64, std::max<long long>(1, (p.NC + 256 * qt - 1) / (256 * qt)));
-    p.CPB = (p.NC + p.G - 1) / p.G;
-    const size_t BG = Bz * (size_t)p.G;
+    auto blocks = [&](long long nc, int &G, long long &cpb) {
+      const long long qt = std::min<long long>(8, std::max<long long>(1, B * nc / (256LL * 256 * 4)));
+      G = (int)std::min<long long>(64, std::max<long long>(1, (nc + 256 * qt - 1) / (256 * qt)));
+      cpb = (nc + G - 1) / G;
+    };
+    blocks(p.NC, p.G, p.CPB);
+    if (!uniform_lanes(B) && B <= 256) {  // group-mode planes (used by smoothing calls)
+      p.NG = (p.NC * B + 255) / 256;
+      blocks(p.NG, p.GG, p.CPBG);
+      p.gagg_off = take(Bz * (size_t)p.NG * elem_len(r) * 8);
+      p.gst_off = take((size_t)p.NG * state_len(r) * Bz * 8);
+      p.gmap_off = take(Bz * (size_t)p.NG * (r * r + r) * 8);
+      p.gms_off = take((size_t)p.NG * r * Bz * 8);
+      p.gnll_off = take((size_t)p.NG * Bz * 8);
+    }
+    p.GF = std::max(p.G, p.GG);
+    const size_t BG = Bz * (size_t)p.GF;
     p.sync_bytes = align256(256 + 3 * BG * 4);
     p.sync_off = take(p.sync_bytes);
     p.agg_off = take(BG * elem_len(r) * 8);
@@ -700,7 +747,8 @@ __global__ __launch_bounds__(kBlock) void k_c0_shared(SmoothArgs a, ChunkPlan p)
 #endif
 // K1 for chunk c of trajectory b
 template <int R, int N, int E, typename T, typename YT, int AI, int CI, bool UNI>
-EKS_DEV void c1_chunk(const SmoothArgs &a, const ChunkPlan &p, long long c, unsigned b) {
+EKS_DEV void c1_chunk(const SmoothArgs &a, const ChunkPlan &p, long long c, unsigned b,
+                      Elem<R> &El) {
   // member prefetch distance (steps); few-trajectory lanes (!UNI: < 1 wave per
   // SIMD, nothing else to hide the HBM latency behind) keep more in flight
   constexpr int D = (E > 0 && E * N <= 16) ? (UNI ? 2 : EKS_C1_DNU) : 1;
@@ -710,7 +758,6 @@ EKS_DEV void c1_chunk(const SmoothArgs &a, const ChunkPlan &p, long long c, unsi
   md.load(a.params + (long long)b * ParamLayout<R, N>::len, first);
   const long long s = c * p.L, e = min(TT, s + p.L);
   bool ok = true;
-  Elem<R> El;
   if (c == 0 && !md.template valid<AI, CI>()) flag(a.status, b, EKS_STATUS_BAD_MODEL);
   if (first) {
     // chunk 0: the plain filter from the prior; summarised as the known
@@ -748,7 +795,6 @@ EKS_DEV void c1_chunk(const SmoothArgs &a, const ChunkPlan &p, long long c, unsi
     });
     if (p.nll_closed) pl((double *)(a.ws + p.nllp_off), c, B, b) = acc.value((double)(e - s) * N);
   }
-  El.store((double *)(a.ws + p.elem_off) + ((long long)b * p.NC + c) * Elem<R>::len, 1);
   if (!ok) flag(a.status, b, first ? EKS_STATUS_SINGULAR : EKS_STATUS_SCAN);
 }
 
@@ -764,8 +810,47 @@ template <int R, int N, int E, typename T, typename YT, int AI, int CI, bool UNI
 EKS_DEV void c1_elem_body(const SmoothArgs &a, const ChunkPlan &p) {
   zero_scan_sync(a, p);
   Lane<UNI> ln;
-  if (!ln.init(a.B, p.NC)) return;
-  c1_chunk<R, N, E, T, YT, AI, CI, UNI>(a, p, ln.c, ln.b);
+  const bool valid = ln.init(a.B, p.NC);
+  double *eplane = (double *)(a.ws + p.elem_off);
+  constexpr int EL = Elem<R>::len;
+  if constexpr (UNI) {
+    if (!valid) return;
+    Elem<R> El;
+    c1_chunk<R, N, E, T, YT, AI, CI, UNI>(a, p, ln.c, ln.b, El);
+    El.store(eplane + ((long long)ln.b * p.NC + ln.c) * EL, 1);
+  } else {
+    Elem<R> El;
+    if (valid)
+      c1_chunk<R, N, E, T, YT, AI, CI, UNI>(a, p, ln.c, ln.b, El);
+    else
+      El.set_identity();
+    if (p.grp) {
+      // group mode: inclusive scan over this trajectory's chunks in the block
+      // (lanes B apart), Hillis-Steele through LDS (dynamic: EL x 256 doubles)
+      extern __shared__ double dsh[];
+      const int tid = threadIdx.x, Bi = (int)a.B;
+      bool ok = true;
+      for (int k = 1; k * Bi < kBlock; k <<= 1) {
+        El.store(dsh + tid, kBlock);
+        __syncthreads();
+        const int j = tid - k * Bi;
+        Elem<R> o;
+        if (j >= 0) o.load(dsh + j, kBlock);
+        __syncthreads();
+        if (j >= 0 && valid) {
+          Elem<R> t;
+          ok = compose_elem<R>(o, El, t) && ok;
+          El = t;
+        }
+      }
+      if (valid) {
+        if (!ok) flag(a.status, ln.b, EKS_STATUS_SCAN);
+        if (tid + Bi >= kBlock || ln.c + 1 == p.NC)  // the group's last chunk: the group total
+          El.store((double *)(a.ws + p.gagg_off) + ((long long)ln.b * p.NG + blockIdx.x) * EL, 1);
+      }
+    }
+    if (valid) El.store(eplane + ((long long)ln.b * p.NC + ln.c) * EL, 1);
+  }
 }
 
 template <int R, int N, int E, typename T, typename YT, int AI, int CI, bool UNI>
@@ -912,7 +997,8 @@ __global__ __launch_bounds__(256) void k_c2_fscan_g(SmoothArgs a, ChunkPlan p) {
   unsigned *fl_tot = p.flags(a.ws, 0, B) + b * G, *fl_nll = p.flags(a.ws, 1, B) + b * G;
   double *aggs = (double *)(a.ws + p.agg_off) + b * G * EL;
   double *parts = (double *)(a.ws + p.part_off) + b * G;
-  const long long cb0 = (long long)g * p.CPB, cb1 = min(NC, cb0 + p.CPB);
+  const long long NCb = p.count_of(b, B);  // NC, or this trajectory's group count
+  const long long cb0 = min(NCb, (long long)g * p.CPB), cb1 = min(NCb, cb0 + p.CPB);
   const long long q = (p.CPB + 255) / 256;
   const long long c0 = min(cb1, cb0 + tid * q), c1 = min(cb1, c0 + q);
   bool ok = true;
@@ -1160,7 +1246,8 @@ __global__ __launch_bounds__(256) void k_c4_bscan_g(SmoothArgs a, ChunkPlan p) {
   unsigned *fl = p.flags(a.ws, 2, B) + b * G;
   double *maggs = (double *)(a.ws + p.magg_off) + b * G * MR;
   double *parts = (double *)(a.ws + p.part_off) + B * G + b * G;
-  const long long cb0 = (long long)g * p.CPB, cb1 = min(NC, cb0 + p.CPB);
+  const long long NCb = p.count_of(b, B);  // NC, or this trajectory's group count
+  const long long cb0 = min(NCb, (long long)g * p.CPB), cb1 = min(NCb, cb0 + p.CPB);
   const long long q = (p.CPB + 255) / 256;
   const long long c0 = min(cb1, cb0 + tid * q), c1 = min(cb1, c0 + q);
   auto load_map = [&](const double *s) {
@@ -1278,7 +1365,7 @@ __global__ __launch_bounds__(256) void k_c4_bscan_g(SmoothArgs a, ChunkPlan p) {
     ms[i] = t;
   }
   map_run([&](long long c, const Affine<R> &f) {
-    if (c + 1 < NC || a.seg_in) {
+    if (c + 1 < NCb || a.seg_in) {
 #pragma unroll
       for (int i = 0; i < R; ++i) msend[(c * R + i) * B + b] = ms[i];
     }
@@ -1470,18 +1557,11 @@ __global__ __launch_bounds__(kBlock) void k_c3_rerun(SmoothArgs a, ChunkPlan p) 
   static_assert(LS % D == 0, "prefetch distance must divide the checkpoint interval");
   Lane<UNI> ln;
   const long long B = a.B, TT = a.T;
-  if (!ln.init(B, p.NC)) return;
-  const long long c = ln.c;
-  const unsigned b = ln.b;
-  constexpr int KS = R + Sym<R>::len;
-  Model<R, N> md;
-  md.load(a.params + (long long)b * ParamLayout<R, N>::len, false);
-  const YT *ybuf = (const YT *)p.ysrc;
-  const double *evbuf = (const double *)p.evsrc;
-  double *ckpt = (double *)(a.ws + p.ckpt_off);
-  double m[R], P[R][R];
-  load_state_pl<R>((const double *)(a.ws + p.cstart_off), c * KS, B, b, m, P);
-  const long long s = c * p.L, e = min(TT, s + p.L);
+  const bool valid = ln.init(B, p.NC);
+  if (UNI || !p.grp) {
+    if (!valid) return;
+  }
+  constexpr int KS = R + Sym<R>::len, MR = R * R + R;
   double G[R][R], g[R];
 #pragma unroll
   for (int i = 0; i < R; ++i) {
@@ -1489,7 +1569,43 @@ __global__ __launch_bounds__(kBlock) void k_c3_rerun(SmoothArgs a, ChunkPlan p) 
 #pragma unroll
     for (int j = 0; j < R; ++j) G[i][j] = (i == j) ? 1.0 : 0.0;
   }
+  double share = 0.0;  // the chunk's NLL share
+  if (valid) {
+  const long long c = ln.c;
+  const unsigned b = ln.b;
+  Model<R, N> md;
+  md.load(a.params + (long long)b * ParamLayout<R, N>::len, false);
+  const YT *ybuf = (const YT *)p.ysrc;
+  const double *evbuf = (const double *)p.evsrc;
+  double *ckpt = (double *)(a.ws + p.ckpt_off);
+  double m[R], P[R][R];
   bool ok = true;
+  if (!UNI && p.grp) {
+    // group mode: the group's start state (K2) composed with the inclusive
+    // prefix K1 stored for the chunk before (same block: lane - B)
+    const double *gst = (const double *)(a.ws + p.gst_off);
+    if (threadIdx.x >= B) {
+      Elem<R> pe;
+      pe.load((const double *)(a.ws + p.elem_off) + ((long long)b * p.NC + c - 1) * Elem<R>::len, 1);
+      if (blockIdx.x == 0) {  // group 0 holds chunk 0, a filtered state (Ab = 0)
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+          m[i] = pe.bb[i];
+#pragma unroll
+          for (int j = 0; j < R; ++j) P[i][j] = pe.Cb[i][j];
+        }
+      } else {
+        load_state_pl<R>(gst, (long long)blockIdx.x * KS, B, b, m, P);
+        ok = compose_state<R>(m, P, pe) && ok;
+      }
+    } else {
+      load_state_pl<R>(gst, (long long)blockIdx.x * KS, B, b, m, P);
+    }
+    if (!ok) flag(a.status, b, EKS_STATUS_SCAN);
+  } else {
+    load_state_pl<R>((const double *)(a.ws + p.cstart_off), c * KS, B, b, m, P);
+  }
+  const long long s = c * p.L, e = min(TT, s + p.L);
   NllAcc acc;
   YT yr[D][N];
   double er[D][N];
@@ -1544,11 +1660,76 @@ __global__ __launch_bounds__(kBlock) void k_c3_rerun(SmoothArgs a, ChunkPlan p) 
       }
     }
   }
-  pl((double *)(a.ws + p.nllp_off), c, B, b) = acc.value((double)(e - s) * N);
+  share = acc.value((double)(e - s) * N);
+  pl((double *)(a.ws + p.nllp_off), c, B, b) = share;
   if (!ok) flag(a.status, b, EKS_STATUS_SINGULAR);
+  }  // valid
   if (!p.smooth) return;
+  if constexpr (!UNI) {
+    if (p.grp) {
+      // group mode: suffix scan of the maps over this trajectory's chunks in
+      // the block (lanes B apart, right to left) and of the NLL shares, in
+      // LDS (dynamic: MR + 1 planes of 256 doubles)
+      extern __shared__ double dsh[];
+      const int tid = threadIdx.x, Bi = (int)B;
+      Affine<R> F;
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        F.g[i] = g[i];
+#pragma unroll
+        for (int j = 0; j < R; ++j) F.G[i][j] = G[i][j];
+      }
+      for (int k = 1; k * Bi < kBlock; k <<= 1) {
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+          dsh[(R * R + i) * kBlock + tid] = F.g[i];
+#pragma unroll
+          for (int j = 0; j < R; ++j) dsh[(i * R + j) * kBlock + tid] = F.G[i][j];
+        }
+        dsh[MR * kBlock + tid] = share;
+        __syncthreads();
+        const int j2 = tid + k * Bi;
+        const bool has = j2 < kBlock && valid && ln.c + k < p.NC;
+        Affine<R> o;
+        double os = 0.0;
+        if (has) {
+#pragma unroll
+          for (int i = 0; i < R; ++i) {
+            o.g[i] = dsh[(R * R + i) * kBlock + j2];
+#pragma unroll
+            for (int j = 0; j < R; ++j) o.G[i][j] = dsh[(i * R + j) * kBlock + j2];
+          }
+          os = dsh[MR * kBlock + j2];
+        }
+        __syncthreads();
+        if (has) {
+          F = F.after(o);
+          share += os;
+        }
+      }
+      if (!valid) return;
+      const unsigned b = ln.b;
+      if (tid < Bi) {  // the group's first chunk: the group totals
+        double *gm = (double *)(a.ws + p.gmap_off) + ((long long)b * p.NG + blockIdx.x) * MR;
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+          gm[R * R + i] = F.g[i];
+#pragma unroll
+          for (int j = 0; j < R; ++j) gm[i * R + j] = F.G[i][j];
+        }
+        pl((double *)(a.ws + p.gnll_off), (long long)blockIdx.x, B, b) = share;
+      }
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        g[i] = F.g[i];
+#pragma unroll
+        for (int j = 0; j < R; ++j) G[i][j] = F.G[i][j];
+      }
+    }
+  }
   // chunk maps are stored trajectory-major: row (b, c) = [G (R*R) | g (R)]
-  double *bw = (double *)(a.ws + p.bwd_off) + ((long long)b * p.NC + c) * (R * R + R);
+  // (group mode: the suffix through the group's last chunk)
+  double *bw = (double *)(a.ws + p.bwd_off) + ((long long)ln.b * p.NC + ln.c) * MR;
 #pragma unroll
   for (int i = 0; i < R; ++i)
 #pragma unroll
@@ -1645,7 +1826,35 @@ __global__ __launch_bounds__(kBlock) void k_c5_final(SmoothArgs a, ChunkPlan p) 
   // ms entering the chunk from the right: from K4, or for the globally last
   // chunk unused (its map ends in the constant mf[T-1]); the last chunk of an
   // earlier time segment gets it from the next segment (eks_smooth_seg)
-  if (c + 1 < p.NC || a.t_base + TT < a.T_total) {
+  if (!UNI && p.grp) {
+    // group mode: the mean entering the group from the right (K4) through
+    // the suffix of the maps after this chunk (K3, same block: lane + B);
+    // the trajectory's last group ends in a constant map (no mean enters)
+#pragma unroll
+    for (int i = 0; i < R; ++i) ms[i] = 0.0;
+    if (c + 1 < p.NC) {
+      const long long blk = blockIdx.x;
+      const bool last_group = ((p.NC - 1) * B + b) / kBlock == blk;
+      double mg[R];
+#pragma unroll
+      for (int i = 0; i < R; ++i)
+        mg[i] = last_group ? 0.0 : pl((const double *)(a.ws + p.gms_off), blk * R + i, B, b);
+      if (threadIdx.x + B < kBlock) {
+        const double *f = (const double *)(a.ws + p.bwd_off) + ((long long)b * p.NC + c + 1) * (R * R + R);
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+          double t = f[R * R + i];
+          if (!last_group)
+#pragma unroll
+            for (int k = 0; k < R; ++k) t = fma(f[i * R + k], mg[k], t);
+          ms[i] = t;
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < R; ++i) ms[i] = mg[i];
+      }
+    }
+  } else if (c + 1 < p.NC || a.t_base + TT < a.T_total) {
     const double *me = (const double *)(a.ws + p.msend_off);
 #pragma unroll
     for (int i = 0; i < R; ++i) ms[i] = pl(me, c * R + i, B, b);
@@ -1769,6 +1978,24 @@ int launch_shape(const SmoothArgs &a, int algo, long long L) {
   const bool shared = !yev && a.sb == 0 && a.B > 1;
   p.yB = shared ? 1 : a.B;
   const bool uni = uniform_lanes(a.B);
+  // group mode: few trajectories, smoothing, whole pipeline, chained scans
+  // (B <= 256: every block but the last holds chunks of every trajectory)
+  p.grp = (!uni && a.B <= kBlock && p.smooth && a.phase == 0 && p.NC > wave_scan_chunks() &&
+           p.NG > 0) ? 1 : 0;
+  const size_t lds1 = p.grp ? (size_t)Elem<R>::len * kBlock * 8 : 0;  // K1's group scan
+  const size_t lds3 = p.grp ? (size_t)(R * R + R + 1) * kBlock * 8 : 0;  // K3's
+  ChunkPlan pg = p, p4 = p;  // K2 / K4 over the group totals
+  if (p.grp) {
+    pg.NC = p4.NC = p.NG;
+    pg.G = p4.G = p.GG;
+    pg.CPB = p4.CPB = p.CPBG;
+    pg.gnc = p4.gnc = p.NC;
+    pg.elem_off = p.gagg_off;
+    pg.cstart_off = p.gst_off;
+    p4.bwd_off = p.gmap_off;
+    p4.msend_off = p.gms_off;
+    p4.nllp_off = p.gnll_off;
+  }
   const unsigned gch = uni ? (unsigned)(p.NC * blocks_per_chunk(a.B))
                            : grid_for(p.NC * a.B, kBlock);
   const unsigned g64 = grid_for(a.B, 64);
@@ -1794,7 +2021,7 @@ int launch_shape(const SmoothArgs &a, int algo, long long L) {
       auto k1 = [&](auto Ec) {
         constexpr int EE = decltype(Ec)::value;
         prof_mark(a.stream, "k_c1_elem");
-        hipLaunchKernelGGL((k_c1_elem<R, N, EE, Tp, YT, AI, CI, U>), dim3(gch), dim3(kBlock), 0,
+        hipLaunchKernelGGL((k_c1_elem<R, N, EE, Tp, YT, AI, CI, U>), dim3(gch), dim3(kBlock), lds1,
                            a.stream, a, p);
         return check_launch("k_c1_elem");
       };
@@ -1823,7 +2050,6 @@ int launch_shape(const SmoothArgs &a, int algo, long long L) {
     // wave per trajectory (log-depth scan) when it is long
     const bool wave_scan = p.NC > wave_scan_chunks();
     const int sw = scan_waves(p.NC);
-    const unsigned gscan = (unsigned)(a.B * p.G);  // k_c2_fscan_g / k_c4_bscan_g blocks
     // the chained scans' sync words: zeroed by K1 in a whole-pipeline call
     auto zero_sync = [&]() -> int {
       if (hipMemsetAsync(a.ws + p.sync_off, 0, p.sync_bytes, a.stream) != hipSuccess)
@@ -1836,7 +2062,8 @@ int launch_shape(const SmoothArgs &a, int algo, long long L) {
       if (!wave_scan)
         hipLaunchKernelGGL((k_c2_fscan<R, N>), dim3(g64), dim3(64), 0, a.stream, a, p);
       else
-        hipLaunchKernelGGL((k_c2_fscan_g<R, N>), dim3(gscan), dim3(256), 0, a.stream, a, p);
+        hipLaunchKernelGGL((k_c2_fscan_g<R, N>), dim3((unsigned)(a.B * pg.G)), dim3(256), 0,
+                           a.stream, a, pg);
       if ((rc = check_launch("k_c2_fscan"))) return rc;
       if (p.nll_fused) {  // K2 summed the closed-form NLL shares: done
         prof_call_end(a.stream);
@@ -1844,7 +2071,7 @@ int launch_shape(const SmoothArgs &a, int algo, long long L) {
       }
       if (!p.nll_closed) {
         prof_mark(a.stream, "k_c3_rerun");
-        hipLaunchKernelGGL((k_c3_rerun<R, N, YT, AI, CI, LS, U>), dim3(gch), dim3(kBlock), 0,
+        hipLaunchKernelGGL((k_c3_rerun<R, N, YT, AI, CI, LS, U>), dim3(gch), dim3(kBlock), lds3,
                            a.stream, a, p);
         if ((rc = check_launch("k_c3_rerun"))) return rc;
       }
@@ -1874,7 +2101,8 @@ int launch_shape(const SmoothArgs &a, int algo, long long L) {
     if (!wave_scan)
       hipLaunchKernelGGL((k_c4_bscan<R>), dim3(g64), dim3(64), 0, a.stream, a, p);
     else
-      hipLaunchKernelGGL((k_c4_bscan_g<R>), dim3(gscan), dim3(256), 0, a.stream, a, p);
+      hipLaunchKernelGGL((k_c4_bscan_g<R>), dim3((unsigned)(a.B * p4.G)), dim3(256), 0, a.stream,
+                         a, p4);
     if ((rc = check_launch("k_c4_bscan"))) return rc;
     prof_mark(a.stream, "k_c5_final");
     hipLaunchKernelGGL((k_c5_final<R, N, YT, AI, CI, LS, U>), dim3(gch), dim3(kBlock), 0,
