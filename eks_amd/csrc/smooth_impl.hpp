@@ -174,6 +174,18 @@ inline long long chunk_len(long long B, long long T, int r) {
   return L;
 }
 
+// (J, d) mode shapes (see ChunkPlan::jd)
+inline bool jd_shape(long long B, int r, int n) {
+  static const int off = [] {  // EKS_NO_JD: tuning experiments only
+    const char *e = getenv("EKS_NO_JD");
+    return e ? atoi(e) : 0;
+  }();
+  // B >= 8: the (J, d) planes are time-major (B values per row); with fewer
+  // trajectories a wave's loads scatter over 64 rows (config 5's B = 1
+  // smooth: K3 + K5 0.20 -> 0.24 ms with them)
+  return !off && !uniform_lanes(B) && B >= 8 && B <= 256 && r >= 3 && n >= 4;
+}
+
 // Chunk length of a smoothing call: with few trajectories (B <= 256,
 // chunk-major lanes) the group-mode scans cost ~the same for any chunk
 // count, so the chunks are as short as the checkpoint grid allows
@@ -235,6 +247,12 @@ struct ChunkPlan {
   int GG = 1;         // G of the group-level scans
   long long CPBG = 0;
   size_t gagg_off = 0, gst_off = 0, gmap_off = 0, gms_off = 0, gnll_off = 0;
+  // (J, d) mode (few trajectories, heavy observation models: r = 3, n >= 4):
+  // K3 stores every step's RTS gain (J_t, d_t) in time-major planes and K5
+  // only runs the backward mean recursion from them, instead of re-running
+  // the filter from checkpoints (config 3: n = 8 dense C)
+  int jd = 0;
+  size_t jd_off = 0;
   // groups of trajectory b in a plan over groups (the last block may not hold b)
   EKS_DEV long long count_of(long long b, long long B) const {
     return gnc ? ((gnc - 1) * B + b) / 256 + 1 : NC;
@@ -264,6 +282,7 @@ inline ChunkPlan make_plan(long long B, long long T, int r, int n, long long L) 
   p.nllp_off = take((size_t)p.NC * Bz * 8);
   p.msend_off = take((size_t)p.NC * r * Bz * 8);
   p.ckpt_off = take((size_t)p.NC * p.NSUB * state_len(r) * Bz * 8);
+  if (jd_shape(B, r, n)) p.jd_off = take((size_t)T * (r * r + r) * Bz * 8);
   if (p.NC > wave_scan_chunks()) {
     // blocks per trajectory: few lanes in all -> ~1 chunk per thread (the
     // scan is latency bound); many -> q chunks per thread so the chip holds
@@ -1538,6 +1557,19 @@ __global__ __launch_bounds__(64) void k_seg_combine(int kind, long long B, int n
   if (!ok && status) atomicOr(status + b, EKS_STATUS_SCAN);
 }
 
+// RTS gain (J_t, d_t) of step t in the (J, d) planes: R*R + R planes per step
+template <int R>
+EKS_DEV void store_jd(double *base, long long t, long long B, unsigned b, const double (&J)[R][R],
+                      const double (&d)[R]) {
+  constexpr int MR = R * R + R;
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    pl(base, t * MR + R * R + i, B, b) = d[i];
+#pragma unroll
+    for (int j = 0; j < R; ++j) pl(base, t * MR + i * R + j, B, b) = J[i][j];
+  }
+}
+
 // y / ev of step t (time-major planes), raw
 template <int N, typename YT>
 EKS_DEV void load_yev(const YT *ybuf, const double *evbuf, long long t, long long B, unsigned b,
@@ -1578,6 +1610,7 @@ __global__ __launch_bounds__(kBlock) void k_c3_rerun(SmoothArgs a, ChunkPlan p) 
   const YT *ybuf = (const YT *)p.ysrc;
   const double *evbuf = (const double *)p.evsrc;
   double *ckpt = (double *)(a.ws + p.ckpt_off);
+  double *jdp = (double *)(a.ws + p.jd_off);
   double m[R], P[R][R];
   bool ok = true;
   if (!UNI && p.grp) {
@@ -1614,7 +1647,7 @@ __global__ __launch_bounds__(kBlock) void k_c3_rerun(SmoothArgs a, ChunkPlan p) 
   for (int q = 0; q < D; ++q) load_yev<N, YT>(ybuf, evbuf, min(s + q, e - 1), p.yB, p.ylane(b), yr[q], er[q]);
   long long k = 0;
   for (long long t0 = s; t0 < e; t0 += LS, ++k) {
-    if (p.smooth) store_state_pl<R>(ckpt, (c * p.NSUB + k) * KS, B, b, m, P);  // state before t0
+    if (p.smooth && !p.jd) store_state_pl<R>(ckpt, (c * p.NSUB + k) * KS, B, b, m, P);  // state before t0
 #pragma unroll
     for (int q = 0; q < LS; ++q) {
       const long long t = t0 + q;
@@ -1632,6 +1665,7 @@ __global__ __launch_bounds__(kBlock) void k_c3_rerun(SmoothArgs a, ChunkPlan p) 
         if (t + a.t_base + 1 < a.T_total) {
           double J[R][R], d[R], GJ[R][R];
           ok = rts_gain<R, AI>(m, P, md.A, md.Q, J, d) && ok;
+          if (p.jd) store_jd<R>(jdp, t, B, b, J, d);
 #pragma unroll
           for (int i = 0; i < R; ++i) {
             double sg = g[i];
@@ -1645,6 +1679,10 @@ __global__ __launch_bounds__(kBlock) void k_c3_rerun(SmoothArgs a, ChunkPlan p) 
 #pragma unroll
             for (int j = 0; j < R; ++j) G[i][j] = GJ[i][j];
         } else {  // ms[T-1] = mf[T-1]: the map ends in a constant
+          if (p.jd) {
+            double Z[R][R] = {};
+            store_jd<R>(jdp, t, B, b, Z, m);
+          }
 #pragma unroll
           for (int i = 0; i < R; ++i) {
             double sg = g[i];
@@ -1809,20 +1847,11 @@ __global__ __launch_bounds__(64) void k_c4_nll(SmoothArgs a, ChunkPlan p) {
   if (l == 0) a.nll[b] = s;
 }
 
-template <int R, int N, typename YT, int AI, int CI, int LS, bool UNI>
-__global__ __launch_bounds__(kBlock) void k_c5_final(SmoothArgs a, ChunkPlan p) {
-  Lane<UNI> ln;
+// the smoothed mean entering chunk c of trajectory b from the right (K5)
+template <int R, bool UNI>
+EKS_DEV void c5_ms_in(const SmoothArgs &a, const ChunkPlan &p, long long c, unsigned b,
+                      double (&ms)[R]) {
   const long long B = a.B, TT = a.T;
-  if (!ln.init(B, p.NC)) return;
-  const long long c = ln.c;
-  const unsigned b = ln.b;
-  constexpr int KS = R + Sym<R>::len;
-  Model<R, N> md;
-  md.load(a.params + (long long)b * ParamLayout<R, N>::len, false);
-  const YT *ybuf = (const YT *)p.ysrc;
-  const double *evbuf = (const double *)p.evsrc;
-  const double *ckpt = (const double *)(a.ws + p.ckpt_off);
-  double ms[R];
   // ms entering the chunk from the right: from K4, or for the globally last
   // chunk unused (its map ends in the constant mf[T-1]); the last chunk of an
   // earlier time segment gets it from the next segment (eks_smooth_seg)
@@ -1862,6 +1891,23 @@ __global__ __launch_bounds__(kBlock) void k_c5_final(SmoothArgs a, ChunkPlan p) 
 #pragma unroll
     for (int i = 0; i < R; ++i) ms[i] = 0.0;
   }
+}
+
+template <int R, int N, typename YT, int AI, int CI, int LS, bool UNI>
+__global__ __launch_bounds__(kBlock) void k_c5_final(SmoothArgs a, ChunkPlan p) {
+  Lane<UNI> ln;
+  const long long B = a.B, TT = a.T;
+  if (!ln.init(B, p.NC)) return;
+  const long long c = ln.c;
+  const unsigned b = ln.b;
+  constexpr int KS = R + Sym<R>::len;
+  Model<R, N> md;
+  md.load(a.params + (long long)b * ParamLayout<R, N>::len, false);
+  const YT *ybuf = (const YT *)p.ysrc;
+  const double *evbuf = (const double *)p.evsrc;
+  const double *ckpt = (const double *)(a.ws + p.ckpt_off);
+  double ms[R];
+  c5_ms_in<R, UNI>(a, p, c, b, ms);
   const long long s = c * p.L, e = min(TT, s + p.L);
   const long long nsub = (e - s + LS - 1) / LS;
   bool ok = true;
@@ -1924,6 +1970,57 @@ __global__ __launch_bounds__(kBlock) void k_c5_final(SmoothArgs a, ChunkPlan p) 
   if (!ok) flag(a.status, b, EKS_STATUS_SINGULAR);
 }
 
+// K5 of (J, d) mode: the backward mean recursion ms_t = J_t ms_{t+1} + d_t
+// over the chunk from the stored gains (K3), D steps of gains in flight
+template <int R, int N, int CI, bool UNI>
+__global__ __launch_bounds__(kBlock) void k_c5_jd(SmoothArgs a, ChunkPlan p) {
+  constexpr int D = 2, MR = R * R + R;
+  Lane<UNI> ln;
+  const long long B = a.B, TT = a.T;
+  if (!ln.init(B, p.NC)) return;
+  const long long c = ln.c;
+  const unsigned b = ln.b;
+  Model<R, N> md;
+  md.load(a.params + (long long)b * ParamLayout<R, N>::len, false);
+  double ms[R];
+  c5_ms_in<R, UNI>(a, p, c, b, ms);
+  const double *jdp = (const double *)(a.ws + p.jd_off);
+  const long long s = c * p.L, e = min(TT, s + p.L);
+  double *outb = a.out + (long long)b * a.ob;
+  double ring[D][MR];
+  auto fetch = [&](int q, long long t) {
+#pragma unroll
+    for (int k = 0; k < MR; ++k) ring[q][k] = pl(jdp, t * MR + k, B, b);
+  };
+  // unconditional loads, step clamped to the chunk's first (see c1_stream)
+#pragma unroll
+  for (int q = 0; q < D; ++q) fetch(q, max(e - 1 - q, s));
+  for (long long t0 = e - 1; t0 >= s; t0 -= D) {
+#pragma unroll
+    for (int q = 0; q < D; ++q) {
+      const long long t = t0 - q;
+      double f[MR];
+#pragma unroll
+      for (int k = 0; k < MR; ++k) f[k] = ring[q][k];
+      fetch(q, max(t - D, s));
+      if (t >= s) {
+        double nx[R];
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+          double sm = f[R * R + i];
+#pragma unroll
+          for (int k = 0; k < R; ++k) sm = fma(f[i * R + k], ms[k], sm);
+          nx[i] = sm;
+        }
+#pragma unroll
+        for (int i = 0; i < R; ++i) ms[i] = nx[i];
+        project_store<R, N, CI>(outb + t * a.ot, a.oj, md.C, ms, md.off);
+        if (a.ms) store_vec<R>(a.ms + ((long long)b * TT + t) * R, ms);
+      }
+    }
+  }
+}
+
 // ===========================================================================
 // host launcher for one (R, N, AI, CI)
 // ===========================================================================
@@ -1984,6 +2081,7 @@ int launch_shape(const SmoothArgs &a, int algo, long long L) {
            p.NG > 0) ? 1 : 0;
   const size_t lds1 = p.grp ? (size_t)Elem<R>::len * kBlock * 8 : 0;  // K1's group scan
   const size_t lds3 = p.grp ? (size_t)(R * R + R + 1) * kBlock * 8 : 0;  // K3's
+  p.jd = (p.jd_off && p.smooth && a.phase == 0) ? 1 : 0;
   ChunkPlan pg = p, p4 = p;  // K2 / K4 over the group totals
   if (p.grp) {
     pg.NC = p4.NC = p.NG;
@@ -2104,6 +2202,12 @@ int launch_shape(const SmoothArgs &a, int algo, long long L) {
       hipLaunchKernelGGL((k_c4_bscan_g<R>), dim3((unsigned)(a.B * p4.G)), dim3(256), 0, a.stream,
                          a, p4);
     if ((rc = check_launch("k_c4_bscan"))) return rc;
+    if (p.jd) {
+      prof_mark(a.stream, "k_c5_jd");
+      hipLaunchKernelGGL((k_c5_jd<R, N, CI, U>), dim3(gch), dim3(kBlock), 0, a.stream, a, p);
+      prof_call_end(a.stream);
+      return check_launch("k_c5_jd");
+    }
     prof_mark(a.stream, "k_c5_final");
     hipLaunchKernelGGL((k_c5_final<R, N, YT, AI, CI, LS, U>), dim3(gch), dim3(kBlock), 0,
                        a.stream, a, p);
