@@ -166,7 +166,11 @@ int64_t eks_param_len(int n, int r);
  *            in the order top x, y, bottom x, y, right x, y, left x, y) and A,
  *            Q are diagonal (:140-147): sparse updates, the two pairs of
  *            equal rows folded into one observation each.  Violations are
- *            flagged in `status`.
+ *            flagged in `status` by the compiled kernels (algos 1-3).  The
+ *            runtime-n kernel (algo 4) runs the general model whatever the
+ *            flags say: it neither uses nor checks them, so it never sets
+ *            EKS_STATUS_BAD_MODEL (its results are those of the general
+ *            model, i.e. correct for any A, C).
  *   workspace / workspace_bytes: device scratch of at least
  *            eks_smooth_workspace_bytes(...) bytes (not zeroed by caller).
  *   algo     0 = automatic, 1 = sequential (one lane per trajectory),
@@ -179,7 +183,9 @@ int64_t eks_param_len(int n, int r);
  *            -- (2, 2) and (3, 4|6|8) are compiled; e.g. the multi-camera
  *            model with V > 4 cameras, n = 2V (the reference accepts any V:
  *            eks/multiview_pca_smoother.py:641-666).  eks_smooth_algo
- *            reports 4 for those shapes.
+ *            reports 4 for those shapes.  One GPU lane per trajectory,
+ *            sequential in time: throughput needs many trajectories (a
+ *            single long trajectory runs on one lane).
  *   status   (B) int32, REQUIRED; zeroed by the call, then bit flags as above.
  */
 size_t eks_smooth_workspace_bytes(int64_t B, int64_t T, int n, int r, int E, int algo);

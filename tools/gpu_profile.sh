@@ -11,7 +11,7 @@ mkdir -p $OUT $RAW
 step() {  # name, timeout, rocprof args...
   local name=$1 t=$2; shift 2
   timeout -k 10 $t rocprofv3 "$@" -d $RAW/$name -o run --output-format csv -- \
-      python3 bench.py --steps ${STEPS:-5} --warmup 1 --no-cpu-baseline > $OUT/$name.log 2>&1
+      python3 bench.py --steps ${STEPS:-5} --warmup 1 --no-cpu-baseline ${BENCH_ARGS} > $OUT/$name.log 2>&1
   local rc=$?
   echo "$name rc=$rc" >> $OUT/status.txt
   (cd $RAW && find $name -type f -printf "%s %p\n") >> $OUT/files.txt
@@ -22,6 +22,6 @@ step() {  # name, timeout, rocprof args...
   return $rc
 }
 RX='k_c[0-9]|k3_|k_model|k_smooth_seq|k_fit'
-step trace 600 --kernel-trace --stats || exit $?
+if [ -z "$NO_TRACE" ]; then step trace 600 --kernel-trace --stats || exit $?; fi
 STEPS=2 step pmc_fetch 600 --kernel-include-regex "$RX" --pmc FETCH_SIZE || exit $?
 STEPS=2 step pmc_write 600 --kernel-include-regex "$RX" --pmc WRITE_SIZE || exit $?
