@@ -781,7 +781,19 @@ extern "C" int eks_fit(const void *obs, int obs_dtype, int64_t B, int64_t T, int
     yo.y = yev;
     yo.ev = (double *)((char *)yev + yev_ev_offset(B, T, n, y32 ? 4 : 8));
   }
-  return dispatch_n(n, [&](auto Nc) {
+  // keypoint observations come in (x, y) pairs: n = 2 (single view) or 2V
+  // (V cameras); the odd n are not compiled (they doubled this unit's code)
+  if (n % 2 != 0 || n > kMaxObs)
+    return set_err(EKS_ERR_UNSUPPORTED, "eks_fit: n=%d not supported (2, 4, 6, 8)", n);
+  auto dispatch_even = [&](auto &&f) -> int {
+    switch (n) {
+      case 2: return f(ic<2>{});
+      case 4: return f(ic<4>{});
+      case 6: return f(ic<6>{});
+      default: return f(ic<8>{});
+    }
+  };
+  return dispatch_even([&](auto Nc) {
     constexpr int NN = decltype(Nc)::value;
     auto by_type = [&](auto tag, auto ytag) -> int {
       using Tp = decltype(tag);
