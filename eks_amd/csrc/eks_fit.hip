@@ -21,9 +21,10 @@
 //                 statistics v_(lo), v_(lo+1) by MSD radix select on the
 //                 IEEE bit patterns (12-bit digits, LDS histograms, early
 //                 exit once the candidate is unique), then numpy's linear
-//                 interpolation -> threshold
-//   k_fit_accum   one lane per (trajectory, chunk): ensemble again, keep
-//                 frames with v_t <= threshold, chunk statistics of y and of
+//                 interpolation -> threshold, and the kept-frame bit mask
+//   k_fit_accum   one lane per (trajectory, chunk): ensemble again (or the y
+//                 hand-off plane + the frame mask), keep frames with
+//                 v_t <= threshold, chunk statistics of y and of
 //                 the differences between consecutive kept frames (shifted
 //                 sums -> mean / scatter matrix), first / last kept y
 //   k_fit_final   one lane per trajectory: merge the chunks in order (Chan
@@ -79,19 +80,6 @@ EKS_DEV void frame_ensemble(const T *p, long long se, long long sj, int Ert, boo
                             double (&y)[N], double &v) {
   double ev[N];
   frame_ensemble<E, N, T>(p, se, sj, Ert, median, y, ev, v);
-}
-
-// the worst (largest) ensemble variance of a frame from its ev values
-template <int N>
-EKS_DEV double worst_of(const double (&ev)[N]) {
-  double v = -1.0;
-  bool nan = false;
-#pragma unroll
-  for (int j = 0; j < N; ++j) {
-    nan |= (ev[j] != ev[j]);
-    v = ev[j] > v ? ev[j] : v;
-  }
-  return nan ? __builtin_nan("") : v;
 }
 
 // y / ev hand-off planes (eks_smooth EKS_YEV32 / EKS_YEV64 input):
@@ -172,20 +160,31 @@ __global__ __launch_bounds__(256) void k_fit_worst(const T *__restrict__ obs, Fi
   }
 }
 
-// Apply f to every key of a row, BLK threads, 8 independent loads in flight
-// per thread (memory-level parallelism for the global-memory passes)
-template <int BLK, typename F>
-EKS_DEV void for_keys(const uint64_t *keys, long long n, F &&f) {
-  constexpr int U = 8;
+// Apply f(key, index) to every key of a row, BLK threads, EKS_SEL_U
+// independent loads in flight per thread (memory-level parallelism for the global-memory
+// passes).  The 64 lanes of a wave always hold 64 consecutive, 64-aligned
+// indices, so a ballot inside f is one word of a frame bit mask.
+#ifndef EKS_SEL_U
+#define EKS_SEL_U 16
+#endif
+template <int BLK, typename K, typename F>
+EKS_DEV void for_keys(const K *keys, long long n, F &&f) {
+  static_assert(BLK % 64 == 0, "whole waves");
+  constexpr int U = EKS_SEL_U;
   long long i = threadIdx.x;
   for (; i + (U - 1) * BLK < n; i += U * BLK) {
-    uint64_t x[U];
+    K x[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) x[u] = keys[i + u * BLK];
 #pragma unroll
-    for (int u = 0; u < U; ++u) f(x[u]);
+    for (int u = 0; u < U; ++u) f(x[u], i + u * BLK);
   }
-  for (; i < n; i += BLK) f(keys[i]);
+  for (; i < n; i += BLK) f(keys[i], i);
+}
+
+// lane 0 of the wave's active lanes (the writer of a ballot word)
+EKS_DEV bool first_active_lane() {
+  return (int)(threadIdx.x & 63) == __ffsll((long long)__ballot(1)) - 1;
 }
 
 // block-wide exclusive prefix sum of one value per thread (BLK threads)
@@ -212,18 +211,25 @@ EKS_DEV long long block_excl_scan(long long x, long long *tmp, long long &total)
 
 // k-th smallest (0-based) key of the row, MSD radix select over the bits
 // below `top` (the keys' common prefix above it is `prefix`).  All threads
-// call it and get the same result.
-template <int BLK>
-EKS_DEV uint64_t block_select(const uint64_t *keys, long long n, long long k, int top,
-                              uint64_t prefix, unsigned *hist, uint64_t *su, long long *si) {
-  uint64_t mask = top >= 63 ? 0ull : ~((2ull << top) - 1);  // bits above `top` fixed
-  for (int hi_bit = top; hi_bit >= 0; hi_bit -= kDigitBits) {
-    const int lo_bit = hi_bit - kDigitBits + 1 > 0 ? hi_bit - kDigitBits + 1 : 0;
+// call it and get the same result.  DB-bit digits: `hist` holds 2^DB bins.
+template <class X>
+struct nodeduce {
+  using type = X;
+};
+
+template <int BLK, int DB = kDigitBits, typename K = uint64_t>
+EKS_DEV K block_select(const K *keys, long long n, long long k, int top,
+                       typename nodeduce<K>::type prefix,
+                       unsigned *hist, uint64_t *su, long long *si) {
+  constexpr int kBitsK = 8 * sizeof(K);
+  K mask = top >= kBitsK - 1 ? K(0) : K(~((K(2) << top) - K(1)));  // bits above `top` fixed
+  for (int hi_bit = top; hi_bit >= 0; hi_bit -= DB) {
+    const int lo_bit = hi_bit - DB + 1 > 0 ? hi_bit - DB + 1 : 0;
     const int bits = hi_bit - lo_bit + 1;
     const unsigned nb = 1u << bits;
     for (unsigned i = threadIdx.x; i < nb; i += blockDim.x) hist[i] = 0;
     __syncthreads();
-    for_keys<BLK>(keys, n, [&](uint64_t x) {
+    for_keys<BLK>(keys, n, [&](K x, long long) {
       if ((x & mask) == prefix) atomicAdd(&hist[(x >> lo_bit) & (nb - 1)], 1u);
     });
     __syncthreads();
@@ -237,24 +243,24 @@ EKS_DEV uint64_t block_select(const uint64_t *keys, long long n, long long k, in
     if (k >= acc && k < acc + mine) {  // exactly one thread
       unsigned d = threadIdx.x * per;
       while (acc + hist[d] <= k) acc += hist[d++];
-      su[0] = prefix | ((uint64_t)d << lo_bit);
+      su[0] = (uint64_t)(prefix | (K(d) << lo_bit));
       si[0] = k - acc;
       si[1] = hist[d];
     }
     __syncthreads();
-    prefix = su[0];
+    prefix = (K)su[0];
     k = si[0];
     const long long left = si[1];
-    mask |= (uint64_t)(nb - 1) << lo_bit;
+    mask |= K(nb - 1) << lo_bit;
     __syncthreads();
     if (left == 1 && lo_bit > 0) {  // the candidate is unique: find it
       if (threadIdx.x == 0) su[1] = ~0ull;
       __syncthreads();
-      for_keys<BLK>(keys, n, [&](uint64_t x) {
-        if ((x & mask) == prefix) atomicMin((unsigned long long *)&su[1], x);
+      for_keys<BLK>(keys, n, [&](K x, long long) {
+        if ((x & mask) == prefix) atomicMin((unsigned long long *)&su[1], (unsigned long long)x);
       });
       __syncthreads();
-      const uint64_t r = su[1];
+      const K r = (K)su[1];
       __syncthreads();
       return r;
     }
@@ -265,23 +271,39 @@ EKS_DEV uint64_t block_select(const uint64_t *keys, long long n, long long k, in
 // One block per trajectory.  Pass 1 histograms the top digit (bits 51-62:
 // exponent and first mantissa bit; variances are >= 0 so bit patterns sort
 // like values) over the row in global memory; pass 2 compacts the keys of
-// the bin holding rank `lo` into LDS; the remaining digits and the
-// neighbouring order statistic are then resolved in LDS.  A bin larger than
-// the LDS buffer falls back to selecting over the global row.
-constexpr int kCand = 4096;  // LDS candidates (32 KB): three blocks per CU
+// the bin holding rank `lo` into LDS (with their frame indices) and sets the
+// kept-frame bits of every frame below that bin; the remaining digits and the
+// neighbouring order statistic are then resolved in LDS, and the bin's own
+// frames are marked against the threshold there.  The frame mask
+// (`kept`, 64 frames per word, trajectory-major, W words per row) is what
+// k_fit_accum reads instead of the ev plane.  A bin larger than the LDS
+// buffer falls back to selecting over the global row, and a row too long for
+// 16-bit indices (or a threshold equal to a key above the bin) marks the
+// frames in one more pass over the row.
+constexpr int kCand = 3072;        // LDS candidates (24 KB + 6 KB of indices)
+constexpr int kSelDigit = 8;       // digits of the in-LDS select (1 KB histogram)
+constexpr long long kLdsMaskT = 65536;  // rows with 16-bit frame indices
 
 template <int BLK>
 __global__ __launch_bounds__(BLK) void k_fit_select(const double *__restrict__ worst,
                                                     long long TT, long long lo, long long hi,
-                                                    double g, double *__restrict__ thr) {
+                                                    double g, double *__restrict__ thr,
+                                                    uint64_t *__restrict__ kept, long long W) {
+  // the top-digit histogram; after the bin is found the same LDS holds the
+  // row's frame mask (T <= kLdsMaskT: at most 1024 words)
   __shared__ unsigned hist[kBins];
+  __shared__ unsigned hsel[1 << kSelDigit];
   __shared__ uint64_t cand[kCand];
+  __shared__ uint16_t cidx[kCand];
   __shared__ uint64_t su[4];
   __shared__ long long si[2 + BLK / 64];
+  __shared__ double sthr;
   __shared__ unsigned ncand;
   __shared__ int any_nan;
+  static_assert(kLdsMaskT / 64 * sizeof(uint64_t) <= sizeof(hist), "mask fits the histogram");
   const long long b = blockIdx.x;
   const uint64_t *keys = reinterpret_cast<const uint64_t *>(worst + b * TT);
+  uint64_t *krow = kept ? kept + b * W : nullptr;
   constexpr int lo_bit = 51;
   for (unsigned i = threadIdx.x; i < kBins; i += BLK) hist[i] = 0;
   if (threadIdx.x == 0) {
@@ -291,7 +313,7 @@ __global__ __launch_bounds__(BLK) void k_fit_select(const double *__restrict__ w
   __syncthreads();
   // pass 1: NaN check + top-digit histogram
   bool nan = false;
-  for_keys<BLK>(keys, TT, [&](uint64_t x) {
+  for_keys<BLK>(keys, TT, [&](uint64_t x, long long) {
     nan |= (x & 0x7fffffffffffffffull) > 0x7ff0000000000000ull;
     atomicAdd(&hist[(x >> lo_bit) & (kBins - 1)], 1u);
   });
@@ -299,6 +321,8 @@ __global__ __launch_bounds__(BLK) void k_fit_select(const double *__restrict__ w
   __syncthreads();
   if (any_nan) {  // np.percentile of an array holding NaN is NaN: no frame kept
     if (threadIdx.x == 0) thr[b] = __builtin_nan("");
+    if (krow)
+      for (long long w = threadIdx.x; w < W; w += BLK) krow[w] = 0ull;
     return;
   }
   // bin of rank lo (parallel scan over the histogram)
@@ -321,13 +345,20 @@ __global__ __launch_bounds__(BLK) void k_fit_select(const double *__restrict__ w
   const long long kin = si[0], cnt_bin = si[1];
   const uint64_t binmask = ~((1ull << lo_bit) - 1);
   __syncthreads();
+  const bool in_lds = cnt_bin <= kCand;
+  const bool lds_mask = krow && in_lds && TT <= kLdsMaskT;
+  uint64_t *smask = reinterpret_cast<uint64_t *>(hist);
   uint64_t ka;
   long long le_in_bin = -1;  // keys of the bin <= ka (when resolved in LDS)
   uint64_t above_in_bin = ~0ull;
-  if (cnt_bin <= kCand) {
-    // pass 2: compact the bin into LDS
+  if (in_lds) {
+    // pass 2: compact the bin into LDS; mask words of the frames below it
     // wave-aggregated slot allocation: one LDS atomic per wave and key batch
-    for_keys<BLK>(keys, TT, [&](uint64_t x) {
+    for_keys<BLK>(keys, TT, [&](uint64_t x, long long i) {
+      if (lds_mask) {
+        const uint64_t mb = __ballot(x < binpfx);  // below the bin: kept
+        if (first_active_lane()) smask[i >> 6] = mb;
+      }
       const bool in = (x & binmask) == binpfx;
       const uint64_t m = __ballot(in);
       if (m == 0) return;
@@ -336,10 +367,13 @@ __global__ __launch_bounds__(BLK) void k_fit_select(const double *__restrict__ w
       unsigned base = 0;
       if (lane == __ffsll((long long)m) - 1) base = atomicAdd(&ncand, (unsigned)__popcll(m));
       base = __shfl(base, __ffsll((long long)m) - 1, 64);
-      if (in) cand[base + below] = x;
+      if (in) {
+        cand[base + below] = x;
+        cidx[base + below] = (uint16_t)i;
+      }
     });
     __syncthreads();
-    ka = block_select<BLK>(cand, cnt_bin, kin, lo_bit - 1, binpfx, hist, su, si);
+    ka = block_select<BLK, kSelDigit>(cand, cnt_bin, kin, lo_bit - 1, binpfx, hsel, su, si);
     if (hi != lo) {
       if (threadIdx.x == 0) {
         su[1] = ~0ull;
@@ -377,7 +411,7 @@ __global__ __launch_bounds__(BLK) void k_fit_select(const double *__restrict__ w
       }
       __syncthreads();
       unsigned long long c = 0, ab = ~0ull;
-      for_keys<BLK>(keys, TT, [&](uint64_t x) {
+      for_keys<BLK>(keys, TT, [&](uint64_t x, long long) {
         c += x <= ka;
         if (x > ka && x < ab) ab = x;
       });
@@ -391,7 +425,27 @@ __global__ __launch_bounds__(BLK) void k_fit_select(const double *__restrict__ w
     const double a = __longlong_as_double((long long)ka);
     const double bb = __longlong_as_double((long long)kb);
     const double d = bb - a;  // numpy's _lerp
-    thr[b] = g >= 0.5 ? bb - d * (1.0 - g) : a + d * g;
+    const double t = g >= 0.5 ? bb - d * (1.0 - g) : a + d * g;
+    thr[b] = t;
+    sthr = t;
+  }
+  if (!krow) return;
+  __syncthreads();
+  const double th = sthr;
+  // every key above the bin is >= kb >= th: kept only when equal to th, which
+  // needs kb above the bin and th == kb (then mark from the global row)
+  const bool amb = (kb & binmask) != binpfx && th >= __longlong_as_double((long long)kb);
+  if (lds_mask && !amb) {
+    for (long long i = threadIdx.x; i < cnt_bin; i += BLK)
+      if (__longlong_as_double((long long)cand[i]) <= th)
+        atomicOr((unsigned long long *)&smask[cidx[i] >> 6], 1ull << (cidx[i] & 63));
+    __syncthreads();
+    for (long long w = threadIdx.x; w < W; w += BLK) krow[w] = smask[w];
+  } else {
+    for_keys<BLK>(keys, TT, [&](uint64_t x, long long i) {
+      const uint64_t m = __ballot(__longlong_as_double((long long)x) <= th);
+      if (first_active_lane()) krow[i >> 6] = m;
+    });
   }
 }
 
@@ -416,7 +470,9 @@ __global__ __launch_bounds__(256) void k_fit_accum(const T *__restrict__ obs, Fi
                                                    long long sb, long long st, long long se,
                                                    long long sj, int Ert, int median,
                                                    const double *__restrict__ thr,
-                                                   double *__restrict__ part, YevOut yi) {
+                                                   const uint64_t *__restrict__ kept,
+                                                   long long W, double *__restrict__ part,
+                                                   YevOut yi) {
   using CS = ChunkStats<N>;
   const long long lane = blockIdx.x * (long long)blockDim.x + threadIdx.x;
   if (lane >= sh.B * sh.NC) return;
@@ -424,6 +480,8 @@ __global__ __launch_bounds__(256) void k_fit_accum(const T *__restrict__ obs, Fi
   const long long t0 = c * sh.Lc, t1 = t0 + sh.Lc < sh.T ? t0 + sh.Lc : sh.T;
   const T *pb = obs + b * sb;
   const double th = thr[b];
+  const uint64_t *krow = FROM_YEV ? kept + b * W : nullptr;
+  uint64_t kw = FROM_YEV ? krow[t0 >> 6] : 0ull;
   // shifted sums: y relative to the chunk's first kept frame K
   double K[N], S1[N], S2[CS::kTri], D1[N], D2[CS::kTri], last[N];
   double cnt = 0.0, npair = 0.0;
@@ -432,19 +490,20 @@ __global__ __launch_bounds__(256) void k_fit_accum(const T *__restrict__ obs, Fi
 #pragma unroll
   for (int i = 0; i < CS::kTri; ++i) S2[i] = D2[i] = 0.0;
   for (long long t = t0; t < t1; ++t) {
-    double y[N], v;
-    if constexpr (FROM_YEV) {  // the ensemble of this frame is already in the planes
-      double ev[N];
+    double y[N];
+    if constexpr (FROM_YEV) {
+      // the ensemble of this frame is already in the y plane, and whether it
+      // is kept in k_fit_select's frame mask (8 of the 24 B per frame that
+      // reading the ev plane took)
+      if ((t & 63) == 0) kw = krow[t >> 6];
+      if (!((kw >> (t & 63)) & 1ull)) continue;
 #pragma unroll
-      for (int j = 0; j < N; ++j) {
-        y[j] = (double)((const YT *)yi.y)[(t * N + j) * sh.B + b];
-        ev[j] = yi.ev[(t * N + j) * sh.B + b];
-      }
-      v = worst_of<N>(ev);
+      for (int j = 0; j < N; ++j) y[j] = (double)((const YT *)yi.y)[(t * N + j) * sh.B + b];
     } else {
+      double v;
       frame_ensemble<E, N, T>(pb + t * st, se, sj, Ert, median != 0, y, v);
+      if (!(v <= th)) continue;
     }
-    if (!(v <= th)) continue;
     if (cnt == 0.0) {
 #pragma unroll
       for (int i = 0; i < N; ++i) K[i] = y[i];
@@ -717,7 +776,9 @@ extern "C" size_t eks_fit_workspace_bytes(int64_t B, int64_t T, int n) {
   fit_chunks(B, T, nc, lc);
   const long long len = 2 + 4LL * n + (long long)n * (n + 1);
   const long long nc2 = (nc + kMergeFan - 1) / kMergeFan;
-  return (size_t)(B * T + B + B * (nc + nc2) * len) * sizeof(double);
+  const long long W = (T + 63) / 64;  // frame-mask words per trajectory
+  // worst plane, thresholds, chunk partials, kept-frame mask
+  return (size_t)(B * T + B + B * (nc + nc2) * len + B * W) * sizeof(double);
 }
 
 // y of the hand-off planes is float32 exactly when it is a member value:
@@ -768,6 +829,9 @@ extern "C" int eks_fit(const void *obs, int obs_dtype, int64_t B, int64_t T, int
   double *thr = worst + B * T;
   double *partA = thr + B;
   double *partB = partA + B * (long long)sh.NC * len;
+  const long long W = (T + 63) / 64;
+  uint64_t *kept = reinterpret_cast<uint64_t *>(
+      partB + B * (long long)((sh.NC + kMergeFan - 1) / kMergeFan) * len);
   // np.percentile 'linear': virtual index (T - 1) q / 100
   const double vi = (double)(T - 1) * (quantile_keep / 100.0);
   const long long lo = (long long)floor(vi);
@@ -807,22 +871,27 @@ extern "C" int eks_fit(const void *obs, int obs_dtype, int64_t B, int64_t T, int
         int rc = check_launch("k_fit_worst");
         if (rc) return rc;
         prof_mark(s, "k_fit_select");
+        // with the hand-off planes written, the selection also writes the
+        // kept-frame mask k_fit_accum reads instead of the ev plane
         if (T >= 65536)
           hipLaunchKernelGGL(k_fit_select<1024>, dim3((unsigned)B), dim3(1024), 0, s, worst, T,
-                             lo, hi, g, thr);
+                             lo, hi, g, thr, yev ? kept : nullptr, W);
         else
           hipLaunchKernelGGL(k_fit_select<256>, dim3((unsigned)B), dim3(256), 0, s, worst, T, lo,
-                             hi, g, thr);
+                             hi, g, thr, yev ? kept : nullptr, W);
         if ((rc = check_launch("k_fit_select"))) return rc;
         prof_mark(s, "k_fit_accum");
-        // with the hand-off planes written, the second pass reads them (24 B
-        // per frame for n = 2) instead of the members (40 B) and skips the sort
+        // with the hand-off planes written, the second pass reads the y plane
+        // and the frame mask (8 B per frame for n = 2 with float32 y) instead
+        // of the members (40 B) and skips the sort
         if (yev)
           hipLaunchKernelGGL((k_fit_accum<EE, NN, Tp, YT, true>), dim3(grid), dim3(256), 0, s,
-                             (const Tp *)obs, sh, sb, st, se, sj, E, median, thr, partA, yo);
+                             (const Tp *)obs, sh, sb, st, se, sj, E, median, thr, kept, W, partA,
+                             yo);
         else
           hipLaunchKernelGGL((k_fit_accum<EE, NN, Tp, YT, false>), dim3(grid), dim3(256), 0, s,
-                             (const Tp *)obs, sh, sb, st, se, sj, E, median, thr, partA, yo);
+                             (const Tp *)obs, sh, sb, st, se, sj, E, median, thr, kept, W, partA,
+                             yo);
         if ((rc = check_launch("k_fit_accum"))) return rc;
         // merge the chunk partials in order, kMergeFan at a time, ping-pong
         double *src = partA, *dst = partB;
