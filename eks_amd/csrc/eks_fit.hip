@@ -290,8 +290,14 @@ __global__ __launch_bounds__(BLK) void k_fit_select(const double *__restrict__ w
                                                     double g, double *__restrict__ thr,
                                                     uint64_t *__restrict__ kept, long long W) {
   // the top-digit histogram; after the bin is found the same LDS holds the
-  // row's frame mask (T <= kLdsMaskT: at most 1024 words)
-  __shared__ unsigned hist[kBins];
+  // row's frame mask (T <= kLdsMaskT: at most 1024 words).  Rows shorter
+  // than 65 536 frames (the 256-thread kernel) count in 16-bit halves of the
+  // words: 8 KB instead of 16, four blocks per CU instead of three.
+  constexpr bool kPacked = BLK == 256;
+  __shared__ unsigned hist[kPacked ? kBins / 2 : kBins];
+  auto hcount = [&](unsigned d) -> unsigned {
+    return kPacked ? (hist[d >> 1] >> ((d & 1u) << 4)) & 0xffffu : hist[d];
+  };
   __shared__ unsigned hsel[1 << kSelDigit];
   __shared__ uint64_t cand[kCand];
   __shared__ uint16_t cidx[kCand];
@@ -305,7 +311,7 @@ __global__ __launch_bounds__(BLK) void k_fit_select(const double *__restrict__ w
   const uint64_t *keys = reinterpret_cast<const uint64_t *>(worst + b * TT);
   uint64_t *krow = kept ? kept + b * W : nullptr;
   constexpr int lo_bit = 51;
-  for (unsigned i = threadIdx.x; i < kBins; i += BLK) hist[i] = 0;
+  for (unsigned i = threadIdx.x; i < (kPacked ? kBins / 2 : kBins); i += BLK) hist[i] = 0;
   if (threadIdx.x == 0) {
     any_nan = 0;
     ncand = 0;
@@ -315,7 +321,11 @@ __global__ __launch_bounds__(BLK) void k_fit_select(const double *__restrict__ w
   bool nan = false;
   for_keys<BLK>(keys, TT, [&](uint64_t x, long long) {
     nan |= (x & 0x7fffffffffffffffull) > 0x7ff0000000000000ull;
-    atomicAdd(&hist[(x >> lo_bit) & (kBins - 1)], 1u);
+    const unsigned d = (unsigned)(x >> lo_bit) & (kBins - 1);
+    if constexpr (kPacked)
+      atomicAdd(&hist[d >> 1], 1u << ((d & 1u) << 4));  // counts <= T < 65 536
+    else
+      atomicAdd(&hist[d], 1u);
   });
   if (nan) any_nan = 1;
   __syncthreads();
@@ -329,15 +339,15 @@ __global__ __launch_bounds__(BLK) void k_fit_select(const double *__restrict__ w
   {
     constexpr unsigned per = kBins / BLK;
     long long mine = 0;
-    for (unsigned d = threadIdx.x * per; d < (threadIdx.x + 1) * per; ++d) mine += hist[d];
+    for (unsigned d = threadIdx.x * per; d < (threadIdx.x + 1) * per; ++d) mine += hcount(d);
     long long total;
     long long acc = block_excl_scan<BLK>(mine, si + 2, total);
     if (lo >= acc && lo < acc + mine) {
       unsigned d = threadIdx.x * per;
-      while (acc + hist[d] <= lo) acc += hist[d++];
+      while (acc + hcount(d) <= lo) acc += hcount(d++);
       su[0] = (uint64_t)d << lo_bit;
       si[0] = lo - acc;
-      si[1] = hist[d];
+      si[1] = hcount(d);
     }
     __syncthreads();
   }
@@ -393,6 +403,8 @@ __global__ __launch_bounds__(BLK) void k_fit_select(const double *__restrict__ w
       above_in_bin = su[1];
       __syncthreads();
     }
+  } else if constexpr (kPacked) {  // the 8 KB histogram holds 2 048 bins: 8-bit digits
+    ka = block_select<BLK, kSelDigit>(keys, TT, lo, 62, 0ull, hsel, su, si);
   } else {
     ka = block_select<BLK>(keys, TT, lo, 62, 0ull, hist, su, si);
   }
