@@ -473,6 +473,21 @@ def workload_pupil(torch, a, dev, rank, world):
                     best_model=[float(x) for x in np.diag(cands[int(state['best'])]['A'])]))
 
 
+def assert_clean(torch, w, where):
+    """Raise if the step's last call flagged any trajectory (singular system,
+    broken model promise, or a scan / chain-wait breakdown: EKS_STATUS_*),
+    plus the workload's own checks.  Run after every loop over the step, so a
+    timed loop never reports a number from a silently failed call."""
+    from eks_amd import batch
+    bad = int((w["status"] != 0).sum().item())
+    if bad:
+        raise RuntimeError(f"{where}: {bad} trajectories reported status bits "
+                           f"(OR = {batch.status_bits(w['status'])}: 1 singular, 2 model "
+                           "promise broken, 4 scan / chain-wait breakdown)")
+    if "post_check" in w:
+        w["post_check"]()
+
+
 def load_pmc(workload_key, path=None):
     """PMC summary of one rank's launch of this workload (tools/gpu_profile.sh
     -> tools/prof_summary.py): bench_pmc.json holds one entry per workload
@@ -608,8 +623,7 @@ def main():
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
-    if int((w["status"] != 0).sum().item()) != 0:
-        raise RuntimeError("singular / mis-flagged trajectories in the bench workload")
+    assert_clean(torch, w, "warm-up")
     # the step's kernel sequence captured once as a HIP graph (hipGraph via
     # torch.cuda.CUDAGraph: the C ABI launches on the capturing stream and
     # allocates nothing), replayed in the timed loop; eager launches if the
@@ -639,8 +653,7 @@ def main():
     dist.barrier()
     elapsed = time.perf_counter() - t0
     elapsed_max = dist.max_over_ranks(elapsed, device=dev)
-    if "post_check" in w:
-        w["post_check"]()
+    assert_clean(torch, w, "timed loop")
     # per-kernel launch durations: HIP events recorded by libeks_hip on the
     # launch stream around each kernel of each eks_smooth call (separate pass,
     # so the events do not perturb the timed loop above)
@@ -648,6 +661,7 @@ def main():
     for _ in range(a.steps):
         eager_step()
     kernels = [(n, ms / a.steps) for n, ms in _lib.profile_end()]  # per step
+    assert_clean(torch, w, "kernel-timing loop")
     kern_ms = sum(ms for _, ms in kernels)
     kern_ms_max = dist.max_over_ranks(kern_ms, device=dev)
     units_local = w["units"]
@@ -670,11 +684,13 @@ def main():
         torch.cuda.synchronize()
         dist.barrier()
         e2e_s = dist.max_over_ranks(time.perf_counter() - f0, device=dev)
+        assert_clean(torch, w, "end-to-end loop")
         _lib.profile_begin(8 * a.steps)
         for _ in range(a.steps):
             fit_step()
             e2e_smooth()
         fit_kernels = [(n, ms / a.steps) for n, ms in _lib.profile_end()]
+        assert_clean(torch, w, "end-to-end kernel-timing loop")
         e2e = dict(value=units_total / e2e_s * a.steps, ms_per_step=e2e_s / a.steps * 1e3,
                    kernels_ms={n: round(ms, 4) for n, ms in fit_kernels},
                    scope="eks_fit (ensemble, good-frame percentile, model fit; writes the "

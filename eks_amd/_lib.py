@@ -23,6 +23,7 @@ EKS_FIT_SINGLEVIEW, EKS_FIT_MULTICAM = 1, 2
 EKS_F32, EKS_F64 = 0, 1
 EKS_YEV32, EKS_YEV64 = 2, 3
 EKS_MEDIAN, EKS_MEAN = 0, 1
+EKS_DBG_WAIT_US, EKS_DBG_A3_SLICE_BYTES = 1, 2
 
 _p = C.c_void_p
 _i64 = C.c_int64
@@ -61,6 +62,7 @@ SIGNATURES = {
     "eks_yev_dtype": (_i32, [_i32, _i32, _i32]),
     "eks_yev_bytes": (_sz, [_i64, _i64, _i32, _i32, _i32, _i32]),
     "eks_interp1d": (_i32, [_p, _i64, _p, _i64, _i64, _i64, _p, _i64, _p, _i64, _i64, _p, _p]),
+    "eks_debug_set": (_i64, [_i32, _i64]),
     "eks_profile_begin": (_i32, [_i32]),
     # include/eks_io.h (host-only)
     "eks_io_last_error": (C.c_char_p, []),
@@ -68,6 +70,11 @@ SIGNATURES = {
     "eks_csv_read": (_i32, [C.c_char_p, _i32, _p, _i64, _i64, _p, _p, _i64, _i32]),
     "eks_profile_end": (_i32, [_p, _p, _i32, _i32]),
 }
+
+
+def debug_set(key: int, value: int) -> int:
+    """eks_debug_set (tests only): returns the previous value."""
+    return int(load().eks_debug_set(key, value))
 
 
 def profile_begin(max_calls: int) -> None:

@@ -41,6 +41,7 @@
 #include "../../include/eks_hip.h"
 #include "eks_common.hpp"
 #include "ensemble.hpp"
+#include "tuning.hpp"
 
 namespace eks {
 
@@ -160,19 +161,21 @@ __global__ __launch_bounds__(256) void k_fit_worst(const T *__restrict__ obs, Fi
   }
 }
 
-// Apply f(key, index) to every key of a row, BLK threads, EKS_SEL_U
+// Apply f(key, index) to every key of a row, BLK threads, kSelU
 // independent loads in flight per thread (memory-level parallelism for the global-memory
 // passes).  The 64 lanes of a wave always hold 64 consecutive, 64-aligned
-// indices, so a ballot inside f is one word of a frame bit mask.
-#ifndef EKS_SEL_U
-#define EKS_SEL_U 16
-#endif
+// indices, so a ballot inside f is one word of a frame bit mask -- as long as
+// the whole wave runs the same loop: the unrolled loop's condition tests the
+// wave's LAST index (i | 63), so near the end of a row a wave never splits
+// between the unrolled body and the tail loop (a split wave would ballot in
+// two halves, and the two writers of the mask word would overwrite each
+// other's frames).
 template <int BLK, typename K, typename F>
 EKS_DEV void for_keys(const K *keys, long long n, F &&f) {
   static_assert(BLK % 64 == 0, "whole waves");
-  constexpr int U = EKS_SEL_U;
+  constexpr int U = kSelU;
   long long i = threadIdx.x;
-  for (; i + (U - 1) * BLK < n; i += U * BLK) {
+  for (; (i | 63) + (U - 1) * BLK < n; i += U * BLK) {
     K x[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) x[u] = keys[i + u * BLK];

@@ -40,6 +40,8 @@ bool use_rt(int r, int n, int algo) {
 
 namespace eks {
 int launch_rt(const SmoothArgs &a);
+long long g_wait_ticks = kDefaultWaitTicks;
+long long g_a3_slice_bytes = 0;
 }
 
 extern "C" {
@@ -119,6 +121,7 @@ static int smooth_call(const void *obs, int obs_dtype, int64_t B, int64_t T, int
   a.phase = phase;
   a.seg_in = seg_in;
   a.seg_out = seg_out;
+  a.wait_ticks = g_wait_ticks;
   if (rt) return launch_rt(a);  // model_flags are promises only: the general kernel serves all
   long long L = (out && phase == 0) ? chunk_len_smooth(B, T, r) : chunk_len(B, T, r);
   if (L >= T) L = (T + 7) / 8 * 8;
@@ -171,6 +174,23 @@ int eks_smooth_seg(const void *obs, int obs_dtype, int64_t B, int64_t T, int E, 
                      phase == 2 && t_base == 0 ? nullptr
                      : (phase == 3 && t_base + T == T_total ? nullptr : seg_in),
                      seg_out);
+}
+
+int64_t eks_debug_set(int key, int64_t value) {
+  clear_err();
+  switch (key) {
+    case EKS_DBG_WAIT_US: {
+      const long long prev = g_wait_ticks < 0 ? -1 : g_wait_ticks / (kWallHz / 1000000);
+      g_wait_ticks = value == 0 ? kDefaultWaitTicks : value < 0 ? -1 : value * (kWallHz / 1000000);
+      return prev;
+    }
+    case EKS_DBG_A3_SLICE_BYTES: {
+      const long long prev = g_a3_slice_bytes;
+      g_a3_slice_bytes = value > 0 ? value : 0;
+      return prev;
+    }
+    default: return set_err(EKS_ERR_ARG, "eks_debug_set: unknown key %d", key), -1;
+  }
 }
 
 int eks_seg_combine(int kind, int64_t B, int nseg, int self, int r, const double *in,

@@ -5,6 +5,15 @@
 // which drains (`s_waitcnt vmcnt(0)`) before one agent-scope flag store; the
 // consumer polls the flag with agent-scope loads and reads the payload with
 // agent-scope (`sc1`, L1-bypassing) loads.
+//
+// Every wait is bounded in wall-clock time (the 100 MHz constant clock read
+// by wall_clock64, independent of the shader clock and of s_sleep's length):
+// a wait that gives up returns false, the caller flags its trajectories
+// EKS_STATUS_SCAN and still publishes, so nothing behind it hangs.  The bound
+// is a kernel argument (SmoothArgs::wait_ticks, default 1 s;
+// eks_debug_set(EKS_DBG_WAIT_US) changes it).  A negative bound is the
+// fault-injection mode of the tests: every wait that would have to poll gives
+// up at once.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -15,6 +24,9 @@ namespace eks {
 typedef __attribute__((address_space(1))) unsigned k3_gu32;
 typedef __attribute__((address_space(1))) unsigned long long k3_gu64;
 
+constexpr long long kWallHz = 100000000LL;  // wall_clock64 rate on gfx950 (hipDeviceAttributeWallClockRate)
+constexpr long long kDefaultWaitTicks = kWallHz;  // 1 s
+
 EKS_DEV void st_wt(double *p, double v) {  // write-through (sc1) store
   __hip_atomic_store((k3_gu64 *)p, __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED,
                      __HIP_MEMORY_SCOPE_AGENT);
@@ -23,21 +35,37 @@ EKS_DEV double ld_wt(const double *p) {  // L1-bypassing (sc1) load
   return __builtin_bit_cast(double, __hip_atomic_load((k3_gu64 *)p, __ATOMIC_RELAXED,
                                                       __HIP_MEMORY_SCOPE_AGENT));
 }
-// publish: every payload store of this wave drained, then one flag store
-EKS_DEV void publish_flag(unsigned *flag, int lane) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (lane == 0) __hip_atomic_store((k3_gu32 *)flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+EKS_DEV unsigned ld_flag(const unsigned *p) {
+  return __hip_atomic_load((k3_gu32 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// wait for a flag (the whole wave polls the one word); false on timeout
-// (~0.1 s: only a bug could get there, and then the call must still end)
-#ifndef EKS_K3_NOWAIT
-#define EKS_K3_NOWAIT 0  // 1: tuning experiment only -- skip the chain waits (wrong results)
-#endif
-EKS_DEV bool wait_flag(const unsigned *flag) {
-  if (EKS_K3_NOWAIT) return true;
-  unsigned spins = 0;
-  while (__hip_atomic_load((k3_gu32 *)flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
-    if (++spins > (1u << 16)) return false;
+// publish: every payload store of this wave drained, then one flag store of
+// value v (1 unless the flag has several states)
+EKS_DEV void publish_flag(unsigned *flag, int lane, unsigned v = 1u) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (lane == 0) __hip_atomic_store((k3_gu32 *)flag, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// a wall-clock deadline for one wait
+struct Deadline {
+  unsigned long long t0 = 0;
+  long long ticks;
+  EKS_DEV explicit Deadline(long long wait_ticks) : ticks(wait_ticks) {}
+  // true once the bound has passed (the first call starts the clock)
+  EKS_DEV bool expired() {
+    if (ticks < 0) return true;
+    const unsigned long long now = wall_clock64();
+    if (t0 == 0) t0 = now;
+    return (long long)(now - t0) > ticks;
+  }
+};
+
+// wait until a flag word is >= v (the whole wave polls the one word);
+// false on timeout
+EKS_DEV bool wait_flag(const unsigned *flag, long long wait_ticks, unsigned v = 1u) {
+  if (wait_ticks < 0) return false;  // fault injection (tests)
+  Deadline dl(wait_ticks);
+  while ((unsigned)__builtin_amdgcn_readfirstlane(ld_flag(flag)) < v) {
+    if (dl.expired()) return false;
     __builtin_amdgcn_s_sleep(2);
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the payload loads below the poll
@@ -46,19 +74,59 @@ EKS_DEV bool wait_flag(const unsigned *flag) {
 
 // every lane with `need` polls its own flag word; returns once all of them
 // are set (false on timeout, as wait_flag)
-EKS_DEV bool wait_flag_lanes(const unsigned *flag, bool need) {
-  if (EKS_K3_NOWAIT) return true;
+EKS_DEV bool wait_flag_lanes(const unsigned *flag, bool need, long long wait_ticks) {
+  if (wait_ticks < 0) return false;  // fault injection (tests)
   bool ready = !need;
-  unsigned spins = 0;
+  Deadline dl(wait_ticks);
   while (true) {
-    if (!ready)
-      ready = __hip_atomic_load((k3_gu32 *)flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+    if (!ready) ready = ld_flag(flag) != 0u;
     if (__all(ready)) break;
-    if (++spins > (1u << 16)) return false;
+    if (dl.expired()) return false;
     __builtin_amdgcn_s_sleep(2);
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   return true;
+}
+
+// Decoupled look-back over a chain of units (flag states: 0 = nothing yet,
+// kAggReady = the unit's own aggregate published, kIncReady = its inclusive
+// value published).  Starting at unit `j` and stepping by `step` (-1: towards
+// earlier units), returns the first unit whose inclusive value is published;
+// every unit passed on the way has its aggregate published.  Units that have
+// published nothing are waited for (each wait bounded as wait_flag); on
+// timeout `ok` is cleared and the search stops at the unit it waited for
+// (whose payload is then stale: the caller's result is flagged, not used).
+// Units published by smaller tickets always publish their aggregate before
+// they wait for anything, so the search ends.
+constexpr unsigned kAggReady = 1u, kIncReady = 2u;
+// the fast path: is unit j's inclusive value already published?
+EKS_DEV bool inc_ready(const unsigned *flag, long long wait_ticks) {
+  if (wait_ticks < 0) return false;  // fault injection: always look back
+  if ((unsigned)__builtin_amdgcn_readfirstlane(ld_flag(flag)) < kIncReady) return false;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  return true;
+}
+EKS_DEV long long look_back(const unsigned *flags, long long j, long long stride, int step,
+                            long long wait_ticks, bool &ok) {
+  if (wait_ticks < 0) {  // fault injection (tests): give up at once
+    ok = false;
+    return j;
+  }
+  while (true) {
+    Deadline dl(wait_ticks);
+    unsigned f;
+    while ((f = (unsigned)__builtin_amdgcn_readfirstlane(ld_flag(flags + j * stride))) == 0u) {
+      if (dl.expired()) {
+        ok = false;
+        return j;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (f >= kIncReady) break;
+    j += step;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  return j;
 }
 
 }  // namespace eks

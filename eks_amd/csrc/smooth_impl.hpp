@@ -44,21 +44,14 @@
 #include "handoff.hpp"
 #include "kf_steps.hpp"
 #include "small_linalg.hpp"
+#include "tuning.hpp"
 
 namespace eks {
 
-// algo 3's member passes stream ~7 GB (config 4) that no cache holds
-// between the two passes: member loads and output stores are non-temporal
-// there (config 4: k3_elem 1.67 -> 1.62, k3_final 1.93 -> 1.87 ms,
-// profiles/r02/nt).  Algo 2 keeps cached loads: its few-trajectory shapes
-// re-read members from the Infinity Cache (config 2 K1 0.046 -> 0.061 ms
-// with non-temporal loads).  0 turns them off (tuning builds).
-#ifndef EKS_NT_LOAD
-#define EKS_NT_LOAD 1
-#endif
-#ifndef EKS_NT_OUT
-#define EKS_NT_OUT 1
-#endif
+
+// debug / fault-injection settings (eks_debug_set; defined in eks_smooth_api.hip)
+extern long long g_wait_ticks;      // chain wait bound (wall_clock64 ticks), < 0: forced timeouts
+extern long long g_a3_slice_bytes;  // algo-3 member offset span per slice (0: 4 GB)
 
 struct SmoothArgs {
   const void *obs;
@@ -85,6 +78,8 @@ struct SmoothArgs {
   int phase = 0;
   const double *seg_in = nullptr;
   double *seg_out = nullptr;
+  // bound of every in-launch chain wait, in wall_clock64 ticks (handoff.hpp)
+  long long wait_ticks = kDefaultWaitTicks;
 };
 
 // Target number of (chunk, trajectory) lanes: enough 256-thread blocks that
@@ -755,22 +750,13 @@ __global__ __launch_bounds__(kBlock) void k_c0_shared(SmoothArgs a, ChunkPlan p)
   }
 }
 
-// few-trajectory prefetch distances of K1 / K3 (config 2: 2 / 4 / 8 steps all
-// within 2 %, tools/c2_dsweep.sh -- these lanes are bound by the per-step FP64
-// dependency chain, not by the load latency)
-#ifndef EKS_C1_DNU
-#define EKS_C1_DNU 2
-#endif
-#ifndef EKS_C3_DNU
-#define EKS_C3_DNU 2
-#endif
 // K1 for chunk c of trajectory b
 template <int R, int N, int E, typename T, typename YT, int AI, int CI, bool UNI>
 EKS_DEV void c1_chunk(const SmoothArgs &a, const ChunkPlan &p, long long c, unsigned b,
                       Elem<R> &El) {
   // member prefetch distance (steps); few-trajectory lanes (!UNI: < 1 wave per
   // SIMD, nothing else to hide the HBM latency behind) keep more in flight
-  constexpr int D = (E > 0 && E * N <= 16) ? (UNI ? 2 : EKS_C1_DNU) : 1;
+  constexpr int D = (E > 0 && E * N <= 16) ? (UNI ? 2 : kC1Dnu) : 1;
   const long long B = a.B, TT = a.T;
   Model<R, N> md;
   const bool first = c == 0 && a.t_base == 0;  // the globally first chunk starts at the prior
@@ -935,11 +921,8 @@ __global__ __launch_bounds__(64) void k_c2_fscan(SmoothArgs a, ChunkPlan p) {
 // loads are unconditional (index clamped into the run: a cache-hit re-read at
 // the tail), so the compiler cannot merge a divergent load into its slot with
 // a copy that waits for it.
-#ifndef EKS_SCAN_PD
-#define EKS_SCAN_PD 1  // config 2 (B = 17, T = 1e5): depth 1 / 2 / 4 -> K2 35 / 39 / 41 us
-#endif
 template <int R>
-constexpr int scan_pd() { return R <= 2 ? EKS_SCAN_PD : 1; }  // r = 3: 27-double elements, 2 would spill at 512 threads
+constexpr int scan_pd() { return R <= 2 ? kScanPd : 1; }  // r = 3: 27-double elements, 2 would spill at 512 threads
 
 // fn(c, element c) for c = c0 .. c1-1 in order; rows of Elem<R>::len doubles
 template <int R, typename F>
@@ -1073,7 +1056,7 @@ __global__ __launch_bounds__(256) void k_c2_fscan_g(SmoothArgs a, ChunkPlan p) {
     if (w == 0) {
       Elem<R> e;
       e.set_identity();
-      if (!wait_flag_lanes(fl_tot + l, l < g)) ok = false;
+      if (!wait_flag_lanes(fl_tot + l, l < g, a.wait_ticks)) ok = false;
       if (l < g) elem_load_wt<R>(e, aggs + (long long)l * EL);
       for (int k = 1; k < g; k <<= 1) {  // levels past g - 1 leave lanes < g alone
         const Elem<R> o = shfl_elem<R, true>(e, k);
@@ -1167,7 +1150,7 @@ __global__ __launch_bounds__(256) void k_c2_fscan_g(SmoothArgs a, ChunkPlan p) {
         if (l == 0) st_wt(parts + g, s);
         publish_flag(fl_nll + g, l);
       } else {  // the last block adds the partial sums in block order
-        if (!wait_flag_lanes(fl_nll + l, l < g)) ok = false;
+        if (!wait_flag_lanes(fl_nll + l, l < g, a.wait_ticks)) ok = false;
         if (l == 0) {
           double tsum = 0.0;
           for (int v = 0; v < g; ++v) tsum += ld_wt(parts + v);
@@ -1346,7 +1329,7 @@ __global__ __launch_bounds__(256) void k_c4_bscan_g(SmoothArgs a, ChunkPlan p) {
       Affine<R> e;
       e.set_identity();
       const bool need = l > g && l < G;
-      if (!wait_flag_lanes(fl + l, need)) ok = false;
+      if (!wait_flag_lanes(fl + l, need, a.wait_ticks)) ok = false;
       if (need) map_load_wt<R>(e, maggs + (long long)l * MR);
       for (int k = 1; k < G - 1 - g; k <<= 1) {  // lane g+1 needs G-1-g lanes
         const Affine<R> o = e.shfl_down(k);
@@ -1585,7 +1568,7 @@ template <int R, int N, typename YT, int AI, int CI, int LS, bool UNI>
 __global__ __launch_bounds__(kBlock) void k_c3_rerun(SmoothArgs a, ChunkPlan p) {
   // y / ev prefetch distance (steps; divides LS): 2 keeps the (2, 2) kernel at
   // 3 waves/SIMD (160 VGPRs), measured 3 % faster than 4 (174 VGPRs, 2 waves)
-  constexpr int D = (R <= 2 && N <= 2) ? (UNI ? 2 : EKS_C3_DNU) : (LS < 4 ? LS : 4);
+  constexpr int D = (R <= 2 && N <= 2) ? (UNI ? 2 : kC3Dnu) : (LS < 4 ? LS : 4);
   static_assert(LS % D == 0, "prefetch distance must divide the checkpoint interval");
   Lane<UNI> ln;
   const long long B = a.B, TT = a.T;

@@ -1,0 +1,33 @@
+// Compile-time tuning constants of the kernels: the measured choices, one
+// place.  (No macro overrides: variant builds for tuning experiments live in
+// tools/, e.g. tools/build_variant.sh on an edited copy of this file.)
+#pragma once
+
+namespace eks {
+
+// algo 3's member passes stream ~7 GB (config 4) that no cache holds between
+// the two passes: member loads and output stores are non-temporal there
+// (config 4: k3_elem 1.67 -> 1.62, k3_final 1.93 -> 1.87 ms, profiles/r02/nt).
+// Algo 2 keeps cached loads: its few-trajectory shapes re-read members from
+// the Infinity Cache (config 2 K1 0.046 -> 0.061 ms with non-temporal loads).
+constexpr bool kNtLoad = true;
+constexpr bool kNtOut = true;
+
+// member prefetch distance (steps) of both algo-3 passes
+constexpr int kK3D = 2;
+
+// few-trajectory prefetch distances of algo 2's K1 / K3 (config 2: 2 / 4 / 8
+// steps all within 2 %, tools/c2_dsweep.sh -- these lanes are bound by the
+// per-step FP64 dependency chain, not by the load latency)
+constexpr int kC1Dnu = 2;
+constexpr int kC3Dnu = 2;
+
+// element / map loads in flight per thread of the chained chunk scans
+// (config 2, B = 17, T = 1e5: depth 1 / 2 / 4 -> K2 35 / 39 / 41 us)
+constexpr int kScanPd = 1;
+
+// independent key loads in flight per thread in eks_fit's selection passes
+// (8 / 16 / 32: 0.91 / 0.85 / 0.86 ms at config 4)
+constexpr int kSelU = 16;
+
+}  // namespace eks

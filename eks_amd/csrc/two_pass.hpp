@@ -70,10 +70,6 @@ constexpr int lds_steps3(int r, int n) {
 }
 constexpr int fine_len3(int r, int n) { return reg_steps3(r, n) + lds_steps3(r, n); }
 
-#ifndef EKS_K3_D
-#define EKS_K3_D 2  // member prefetch distance (steps) of both passes
-#endif
-
 struct Plan3 {
   // NCc / units: k3_bwd's 4-chunk units; NCu / units_f: k3_fwd's (4 x FPW)
   long long L = 16, NCf = 0, NCc = 0, NCu = 0, ng = 0, units = 0, units_f = 0;
@@ -81,6 +77,8 @@ struct Plan3 {
   // then one flag word per unit for each pass
   size_t sync_bytes = 0, flag1_off = 0, flag2_off = 0;
   size_t fst_off = 0, inc2_off = 0, nllp_off = 0, prm_off = 0, total = 0;
+  // look-back aggregates: k3_fwd's unit elements, k3_bwd's 4 chunk maps per unit
+  size_t agg1_off = 0, agg2_off = 0;
 };
 
 inline Plan3 make_plan3(long long B, long long T, int r, int n) {
@@ -110,6 +108,11 @@ inline Plan3 make_plan3(long long B, long long T, int r, int n) {
   p.inc2_off = take((size_t)p.NCc * r * Bz * 8);
   p.nllp_off = take((size_t)p.NCf * Bz * 8);
   p.prm_off = take((size_t)param_len(n, r) * Bz * 8);  // k_model_planes
+  // a unit's aggregate, published for the look-back of later units when the
+  // value it waits for is not there yet: k3_fwd's element of unit c (planes
+  // c * EL ..), k3_bwd's 4 RTS maps of unit c (planes (c * kWV + v) * MP ..)
+  p.agg1_off = take((size_t)p.NCu * elem_len(r) * Bz * 8);
+  p.agg2_off = take((size_t)p.NCc * kWV * (r * r + r) * Bz * 8);
   p.total = off;
   return p;
 }
@@ -126,7 +129,7 @@ EKS_DEV __amdgpu_buffer_rsrc_t member_rsrc(const void *p) {
 }
 template <typename T>
 EKS_DEV T member_load(__amdgpu_buffer_rsrc_t rs, unsigned voff, int soff) {
-  constexpr int aux = EKS_NT_LOAD ? 2 : 0;  // nt: streamed once
+  constexpr int aux = kNtLoad ? 2 : 0;  // nt: streamed once
   if constexpr (sizeof(T) == 4)
     return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(rs, voff, soff, aux));
   else
@@ -192,13 +195,13 @@ struct YevRing {
   EKS_DEV void fetch(int slot, long long t) {
 #pragma unroll
     for (int j = 0; j < N; ++j) {
-#if EKS_NT_LOAD
-      y[slot][j] = __builtin_nontemporal_load(&pl(yb, t * N + j, B, b));
-      ev[slot][j] = __builtin_nontemporal_load(&pl(eb, t * N + j, B, b));
-#else
-      y[slot][j] = pl(yb, t * N + j, B, b);
-      ev[slot][j] = pl(eb, t * N + j, B, b);
-#endif
+      if constexpr (kNtLoad) {
+        y[slot][j] = __builtin_nontemporal_load(&pl(yb, t * N + j, B, b));
+        ev[slot][j] = __builtin_nontemporal_load(&pl(eb, t * N + j, B, b));
+      } else {
+        y[slot][j] = pl(yb, t * N + j, B, b);
+        ev[slot][j] = pl(eb, t * N + j, B, b);
+      }
     }
   }
   EKS_DEV void get(int slot, double (&avg)[N], double (&rv)[N]) const {
@@ -218,6 +221,63 @@ template <int E, int N, typename YT, int D>
 struct SrcOf<E, N, YevIn<YT>, D> {
   using type = YevRing<N, YT, D>;
 };
+
+// Look-back payloads in time-major planes, stored write-through / loaded
+// L1-bypassing (handoff.hpp).
+template <int R>
+EKS_DEV void elem_store_pl_wt(const Elem<R> &E, double *base, long long plane0, long long B,
+                              unsigned b) {
+  double v[Elem<R>::len];
+  E.store(v, 1);
+#pragma unroll
+  for (int k = 0; k < Elem<R>::len; ++k) st_wt(&pl(base, plane0 + k, B, b), v[k]);
+}
+template <int R>
+EKS_DEV void elem_load_pl_wt(Elem<R> &E, const double *base, long long plane0, long long B,
+                             unsigned b) {
+  double v[Elem<R>::len];
+#pragma unroll
+  for (int k = 0; k < Elem<R>::len; ++k) v[k] = ld_wt(&pl(base, plane0 + k, B, b));
+  E.load(v, 1);
+}
+template <int R>
+EKS_DEV void state_load_pl_wt(const double *base, long long plane0, long long B, unsigned b,
+                              double (&m)[R], double (&P)[R][R]) {
+  int k = 0;
+#pragma unroll
+  for (int i = 0; i < R; ++i) m[i] = ld_wt(&pl(base, plane0 + (k++), B, b));
+#pragma unroll
+  for (int i = 0; i < R; ++i)
+#pragma unroll
+    for (int j = i; j < R; ++j) P[i][j] = P[j][i] = ld_wt(&pl(base, plane0 + (k++), B, b));
+}
+template <int R>
+EKS_DEV void state_store_pl_wt(double *base, long long plane0, long long B, unsigned b,
+                               const double (&m)[R], const double (&P)[R][R]) {
+  int k = 0;
+#pragma unroll
+  for (int i = 0; i < R; ++i) st_wt(&pl(base, plane0 + (k++), B, b), m[i]);
+#pragma unroll
+  for (int i = 0; i < R; ++i)
+#pragma unroll
+    for (int j = i; j < R; ++j) st_wt(&pl(base, plane0 + (k++), B, b), P[i][j]);
+}
+// ms <- G ms + g (the one expression every application of a chunk map uses,
+// so that a mean carried through any number of maps has the same bits
+// whichever unit applies them)
+template <int R>
+EKS_DEV void apply_map(const double (&G)[R][R], const double (&g)[R], double (&ms)[R]) {
+  double nx[R];
+#pragma unroll
+  for (int u = 0; u < R; ++u) {
+    double sm = g[u];
+#pragma unroll
+    for (int q = 0; q < R; ++q) sm = fma(G[u][q], ms[q], sm);
+    nx[u] = sm;
+  }
+#pragma unroll
+  for (int u = 0; u < R; ++u) ms[u] = nx[u];
+}
 
 // The first D steps of a lane's chunk into the ring (issued ahead: for the
 // next unit while the current one finishes its tail).
@@ -299,7 +359,7 @@ constexpr int fwd_fpw() { return R <= 2 ? 2 : 1; }
 template <int R, int N, int E, typename T, int AI, int CI>
 __global__ __launch_bounds__(64 * kWV) void k3_fwd(SmoothArgs a, Plan3 p) {
   constexpr int EL = Elem<R>::len, KS = R + Sym<R>::len;
-  constexpr int D = EKS_K3_D;
+  constexpr int D = kK3D;
   constexpr int LF = fine_len3(R, N);
   constexpr int FPW = fwd_fpw<R>(), KPU = kWV * FPW;
   __shared__ double shA[FPW > 1 ? kWV : 1][EL][64];  // each wave's first element (FPW = 2)
@@ -311,6 +371,7 @@ __global__ __launch_bounds__(64 * kWV) void k3_fwd(SmoothArgs a, Plan3 p) {
   unsigned *ctr = (unsigned *)a.ws;
   unsigned *flags = (unsigned *)(a.ws + p.flag1_off);
   double *fst = (double *)(a.ws + p.fst_off);
+  double *agg1 = (double *)(a.ws + p.agg1_off);
   const double *prm = (const double *)(a.ws + p.prm_off);
   typename SrcOf<E, N, T, D>::type src;  // member ring, persists across units
   src.init(a);
@@ -459,8 +520,14 @@ __global__ __launch_bounds__(64 * kWV) void k3_fwd(SmoothArgs a, Plan3 p) {
       ok = compose_elem<R>(Ea, Eb, Ec) && ok;
     }
     if (w == 0) {
-      // the chain: filtered state entering unit cu, published by the unit
-      // before it (for cu = 0 any state: chunk 0's element has Ab = 0)
+      // the chain: filtered state entering unit cu = the state leaving unit
+      // cu - 1 (for cu = 0 any state: chunk 0's element has Ab = 0).
+      // Decoupled look-back: if unit cu - 1 has not published that state yet,
+      // this unit publishes its own element for the units after it, then walks
+      // back to the nearest unit j whose leaving state is published and folds
+      // the elements of units j+1 .. cu-1 into it.  compose_state is a left
+      // fold of state (x) element, so the state has the same bits whichever j
+      // it starts from: results do not depend on timing.
       double m[R], P[R][R];
 #pragma unroll
       for (int i = 0; i < R; ++i) {
@@ -469,16 +536,22 @@ __global__ __launch_bounds__(64 * kWV) void k3_fwd(SmoothArgs a, Plan3 p) {
         for (int j = 0; j < R; ++j) P[i][j] = 0.0;
       }
       if (cu > 0) {
-        if (!wait_flag(flags + (cu - 1) * p.ng + grp)) ok = false;
+        const unsigned *fl = flags + grp;
+        long long j = cu - 1;
+        if (!inc_ready(fl + j * p.ng, a.wait_ticks)) {
+          if (cu + 1 < p.NCu) {
+            if (lane_ok) elem_store_pl_wt<R>(Ec, agg1, cu * EL, B, b);
+            publish_flag(flags + cu * p.ng + grp, l, kAggReady);
+          }
+          j = look_back(fl, j, p.ng, -1, a.wait_ticks, ok);
+        }
         if (lane_ok) {
-          int k = 0;
-          const long long pl0 = (cu * KPU) * KS;
-#pragma unroll
-          for (int i = 0; i < R; ++i) m[i] = ld_wt(&pl(fst, pl0 + (k++), B, b));
-#pragma unroll
-          for (int i = 0; i < R; ++i)
-#pragma unroll
-            for (int j = i; j < R; ++j) P[i][j] = P[j][i] = ld_wt(&pl(fst, pl0 + (k++), B, b));
+          state_load_pl_wt<R>(fst, ((j + 1) * KPU) * KS, B, b, m, P);
+          for (long long i = j + 1; i < cu; ++i) {
+            Elem<R> Ei;
+            elem_load_pl_wt<R>(Ei, agg1, i * EL, B, b);
+            ok = compose_state<R>(m, P, Ei) && ok;
+          }
         }
       }
       {
@@ -492,17 +565,8 @@ __global__ __launch_bounds__(64 * kWV) void k3_fwd(SmoothArgs a, Plan3 p) {
       }
       ok = compose_state<R>(m, P, Ec) && ok;  // the state leaving unit cu
       if (cu + 1 < p.NCu) {
-        if (lane_ok) {
-          int k = 0;
-          const long long pl0 = ((cu + 1) * KPU) * KS;
-#pragma unroll
-          for (int i = 0; i < R; ++i) st_wt(&pl(fst, pl0 + (k++), B, b), m[i]);
-#pragma unroll
-          for (int i = 0; i < R; ++i)
-#pragma unroll
-            for (int j = i; j < R; ++j) st_wt(&pl(fst, pl0 + (k++), B, b), P[i][j]);
-        }
-        publish_flag(flags + cu * p.ng + grp, l);
+        if (lane_ok) state_store_pl_wt<R>(fst, ((cu + 1) * KPU) * KS, B, b, m, P);
+        publish_flag(flags + cu * p.ng + grp, l, kIncReady);
       }
       head(tn);
     }
@@ -542,7 +606,7 @@ __global__ __launch_bounds__(64 * kWV) void k3_fwd(SmoothArgs a, Plan3 p) {
 template <int R, int N, int E, typename T, int AI, int CI, bool NLL>
 __global__ __launch_bounds__(64 * kWV) void k3_bwd(SmoothArgs a, Plan3 p) {
   constexpr int KS = R + Sym<R>::len, MP = R * R + R;
-  constexpr int D = EKS_K3_D;
+  constexpr int D = kK3D;
   constexpr int NR = reg_steps3(R, N), NL = lds_steps3(R, N), LF = NR + NL;
   __shared__ double fs[NL][KS][64 * kWV];  // filtered states of the first NL steps
   __shared__ double shM[kWV - 1][MP][64];  // RTS maps of waves 1..3, then their entering means
@@ -554,6 +618,7 @@ __global__ __launch_bounds__(64 * kWV) void k3_bwd(SmoothArgs a, Plan3 p) {
   unsigned *flags = (unsigned *)(a.ws + p.flag2_off);
   const double *fst = (const double *)(a.ws + p.fst_off);
   double *inc = (double *)(a.ws + p.inc2_off);
+  double *agg2 = (double *)(a.ws + p.agg2_off);
   const double *prm = (const double *)(a.ws + p.prm_off);
   const bool vec2 = N == 2 && a.oj == 1 && ((a.ob | a.ot) & 1) == 0 &&
                     (((uintptr_t)a.out) & 15) == 0;
@@ -683,52 +748,82 @@ __global__ __launch_bounds__(64 * kWV) void k3_bwd(SmoothArgs a, Plan3 p) {
     double ms[R];  // smoothed mean at the first step after this chunk
     if (w == 0) {
       // the chain: the mean at the first step of coarse chunk cc+1, published
-      // by its unit (for the last coarse chunk: unused, its last map is constant)
+      // by its unit (for the last coarse chunk: unused, its last map is
+      // constant).  Decoupled look-back as in k3_fwd: if unit cc+1 has not
+      // published it yet, this unit publishes its 4 maps for the units before
+      // it, walks forward to the nearest unit j with a published mean and
+      // carries that mean back through the maps of units j-1 .. cc+1, right
+      // to left, with the expression the units themselves use (apply_map):
+      // the same bits whichever j it starts from.
 #pragma unroll
       for (int u = 0; u < R; ++u) ms[u] = 0.0;
       if (cc + 1 < p.NCc) {
-        if (!wait_flag(flags + (cc + 1) * p.ng + grp)) okc = false;
-        if (lane_ok)
+        const unsigned *fl = flags + grp;
+        long long j = cc + 1;
+        if (!inc_ready(fl + j * p.ng, a.wait_ticks)) {
+          if (cc > 0) {
+            if (lane_ok) {
+              double *mp0 = agg2;
+              const long long base = cc * kWV * MP;
 #pragma unroll
-          for (int u = 0; u < R; ++u) ms[u] = ld_wt(&pl(inc, (cc + 1) * R + u, B, b));
+              for (int u = 0; u < R; ++u) {
+#pragma unroll
+                for (int q = 0; q < R; ++q) st_wt(&pl(mp0, base + u * R + q, B, b), Mp.G[u][q]);
+                st_wt(&pl(mp0, base + R * R + u, B, b), Mp.g[u]);
+              }
+#pragma unroll
+              for (int v = 1; v < kWV; ++v)
+#pragma unroll
+                for (int k = 0; k < MP; ++k)
+                  st_wt(&pl(mp0, base + v * MP + k, B, b), shM[v - 1][k][l]);
+            }
+            publish_flag(flags + cc * p.ng + grp, l, kAggReady);
+          }
+          j = look_back(fl, j, p.ng, +1, a.wait_ticks, okc);
+        }
+        if (lane_ok) {
+#pragma unroll
+          for (int u = 0; u < R; ++u) ms[u] = ld_wt(&pl(inc, j * R + u, B, b));
+          for (long long i = j - 1; i > cc; --i) {
+#pragma unroll
+            for (int v = kWV - 1; v >= 0; --v) {
+              double G[R][R], g[R];
+              const long long base = (i * kWV + v) * MP;
+#pragma unroll
+              for (int u = 0; u < R; ++u) {
+#pragma unroll
+                for (int q = 0; q < R; ++q) G[u][q] = ld_wt(&pl(agg2, base + u * R + q, B, b));
+                g[u] = ld_wt(&pl(agg2, base + R * R + u, B, b));
+              }
+              apply_map<R>(G, g, ms);
+            }
+          }
+        }
       }
       // right to left through waves 3, 2, 1: hand each its entering mean
 #pragma unroll
       for (int v = kWV - 1; v >= 1; --v) {
-        Affine<R> Mv;
+        double G[R][R], g[R];
         int k = 0;
 #pragma unroll
         for (int u = 0; u < R; ++u)
 #pragma unroll
-          for (int q = 0; q < R; ++q) Mv.G[u][q] = shM[v - 1][k++][l];
+          for (int q = 0; q < R; ++q) G[u][q] = shM[v - 1][k++][l];
 #pragma unroll
-        for (int u = 0; u < R; ++u) Mv.g[u] = shM[v - 1][k++][l];
+        for (int u = 0; u < R; ++u) g[u] = shM[v - 1][k++][l];
 #pragma unroll
         for (int u = 0; u < R; ++u) shM[v - 1][u][l] = ms[u];
-        double nx[R];
-#pragma unroll
-        for (int u = 0; u < R; ++u) {
-          double sm = Mv.g[u];
-#pragma unroll
-          for (int q = 0; q < R; ++q) sm = fma(Mv.G[u][q], ms[q], sm);
-          nx[u] = sm;
-        }
-#pragma unroll
-        for (int u = 0; u < R; ++u) ms[u] = nx[u];
+        apply_map<R>(G, g, ms);
       }
       if (cc > 0) {  // the mean at this coarse chunk's first step
         double x[R];
 #pragma unroll
-        for (int u = 0; u < R; ++u) {
-          double sm = Mp.g[u];
-#pragma unroll
-          for (int q = 0; q < R; ++q) sm = fma(Mp.G[u][q], ms[q], sm);
-          x[u] = sm;
-        }
+        for (int u = 0; u < R; ++u) x[u] = ms[u];
+        apply_map<R>(Mp.G, Mp.g, x);
         if (lane_ok)
 #pragma unroll
           for (int u = 0; u < R; ++u) st_wt(&pl(inc, cc * R + u, B, b), x[u]);
-        publish_flag(flags + cc * p.ng + grp, l);
+        publish_flag(flags + cc * p.ng + grp, l, kIncReady);
       }
     }
     __syncthreads();
@@ -752,12 +847,12 @@ __global__ __launch_bounds__(64 * kWV) void k3_bwd(SmoothArgs a, Plan3 p) {
                 cm[j] = u + md.off[j];
               }
             }
-#if EKS_NT_OUT  // streaming (non-temporal) output stores (smooth_impl.hpp)
-            __builtin_nontemporal_store(cm[0], outb + tt * a.ot);
-            __builtin_nontemporal_store(cm[1], outb + tt * a.ot + 1);
-#else
-            *(double2 *)(outb + tt * a.ot) = make_double2(cm[0], cm[1]);
-#endif
+            if constexpr (kNtOut) {  // streaming (non-temporal) output stores
+              __builtin_nontemporal_store(cm[0], outb + tt * a.ot);
+              __builtin_nontemporal_store(cm[1], outb + tt * a.ot + 1);
+            } else {
+              *(double2 *)(outb + tt * a.ot) = make_double2(cm[0], cm[1]);
+            }
           } else {
             project_store<R, N, CI>(outb + tt * a.ot, a.oj, md.C, ms, md.off);
           }
@@ -915,7 +1010,10 @@ int launch_algo3(const SmoothArgs &a) {
   const long long per = yev ? 0 : a.sb * esz;  // bytes between trajectories
   // the largest member / coordinate offset of a step (buffer soffset)
   const long long soff = yev ? 0 : ((a.E - 1) * a.se + (N - 1) * a.sj) * esz + esz;
-  const long long lim = (1LL << 32) - soff;
+  // (eks_debug_set(EKS_DBG_A3_SLICE_BYTES) lowers the 4 GB span: tests of the slicing)
+  const long long span = g_a3_slice_bytes > 0 && g_a3_slice_bytes < (1LL << 32) ? g_a3_slice_bytes
+                                                                               : (1LL << 32);
+  const long long lim = span - soff;
   if (per <= 0 || (a.B - 1) * per < lim) return launch_algo3_one<R, N, AI, CI>(a);
   const long long cap = std::max(1LL, lim / per);  // trajectories per slice
   if (lim <= 0)

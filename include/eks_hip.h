@@ -310,6 +310,22 @@ int eks_interp1d(const double *x, int64_t nx, const double *y, int64_t ncol, int
                  int64_t so_col, int32_t *status, void *stream);
 
 /*
+ * Test and fault-injection settings (process-wide, not part of the
+ * smoother's semantics; tests only).  Returns the previous value.
+ *   EKS_DBG_WAIT_US        bound of every in-launch chain wait of the
+ *                          time-parallel passes, in microseconds of wall-clock
+ *                          time (0 = the default, 1 s).  A wait that reaches
+ *                          it gives up, flags its trajectories EKS_STATUS_SCAN
+ *                          and lets the launch finish.  -1 = every wait gives
+ *                          up at once (drives the time-out path).
+ *   EKS_DBG_A3_SLICE_BYTES largest member byte offset span of one algo-3
+ *                          launch (0 = 4 GB, the buffer descriptor's range);
+ *                          a smaller span forces the batch slicing.
+ */
+enum { EKS_DBG_WAIT_US = 1, EKS_DBG_A3_SLICE_BYTES = 2 };
+int64_t eks_debug_set(int key, int64_t value);
+
+/*
  * Profiling aid (not part of the smoother's semantics).  After
  * eks_profile_begin(max_calls), each eks_smooth call on this thread records
  * a hipEvent on its stream before each of its kernels and after the last one

@@ -70,9 +70,14 @@ def test_mask_ties_quantised_members(torch, q):
     _vs_host(st, p, q)
 
 
-@pytest.mark.parametrize("T", [2, 63, 64, 65, 1000, 4097])
+@pytest.mark.parametrize("T", [2, 63, 64, 65, 1000, 4000, 4097, 8010, 81000])
 def test_mask_row_lengths(torch, T):
-    """Rows shorter than a wave, exactly one word, ragged last words."""
+    """Rows shorter than a wave, exactly one word, ragged last words; and
+    lengths where the last unrolled round of the selection's key loop ends
+    inside a wave (T in (3840 + 4096 k, 4096 + 4096 k), T % 64 != 0 for the
+    256-thread kernel: 4000, 8010; 81000 for the 1024-thread one): a wave
+    split between the unrolled loop and the tail would ballot its mask word
+    in two halves that overwrite each other (eks_fit.hip for_keys)."""
     from eks_amd import synthetic
     rng = np.random.default_rng(T)
     st = np.stack([synthetic.singleview_obs(rng, 3, T)[:, :, 0] for _ in range(5)])
