@@ -10,6 +10,11 @@ then all objects are linked into one shared library with a plain C ABI
 (include/eks_hip.h).  The library is what the Python package binds with
 ctypes; it is built in the tree so that it travels with the repository
 snapshot to the GPU box.
+
+A second library, ``libeks_torch.so``, registers the same entry points as
+PyTorch operators in C++ (``csrc/torch_ops.cpp``: TORCH_LIBRARY(eks, ...),
+CUDA-key and Meta kernels); it is compiled against the installed torch's
+headers and links libeks_hip.so (``eks_amd.ops`` loads it).
 """
 from __future__ import annotations
 
@@ -27,6 +32,8 @@ CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "lib")
 OBJDIR = os.path.join(LIBDIR, "obj")
 LIBNAME = "libeks_hip.so"
+TORCH_LIBNAME = "libeks_torch.so"
+TORCH_SRC = "torch_ops.cpp"
 ARCH = os.environ.get("EKS_OFFLOAD_ARCH", "gfx950")
 HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 # EKS_EXTRA_CFLAGS: tuning experiments only (e.g. "-DEKS_K3_D=2"), not used by default
@@ -37,6 +44,43 @@ CFLAGS = [*EXTRA, "-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall
 
 def lib_path() -> str:
     return os.path.join(LIBDIR, LIBNAME)
+
+
+def torch_lib_path() -> str:
+    return os.path.join(LIBDIR, TORCH_LIBNAME)
+
+
+def _torch_flags():
+    """Compile / link flags of a host-only C++ unit against the installed
+    PyTorch-ROCm (what torch.utils.cpp_extension would pass)."""
+    import torch
+    from torch.utils import cpp_extension
+    tdir = os.path.dirname(torch.__file__)
+    inc = [f"-I{p}" for p in cpp_extension.include_paths()] + ["-I/opt/rocm/include"]
+    abi = int(bool(torch._C._GLIBCXX_USE_CXX11_ABI))
+    cflags = ["-O2", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
+              f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
+              *inc]
+    ldflags = [f"-L{os.path.join(tdir, 'lib')}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu",
+               "-ltorch_hip", "-lamdhip64", f"-L{LIBDIR}", "-leks_hip", "-Wl,-rpath,$ORIGIN"]
+    return cflags, ldflags
+
+
+def build_torch_ops(force: bool = False, verbose: bool = True) -> str:
+    """libeks_torch.so: torch.ops.eks.* registered in C++ (csrc/torch_ops.cpp)."""
+    src = os.path.join(CSRC, TORCH_SRC)
+    out = torch_lib_path()
+    if not force and not _stale(out, [src, lib_path(), *glob.glob(os.path.join(REPO, "include", "*.h"))]):
+        return out
+    cflags, ldflags = _torch_flags()
+    cmd = [CXX, *cflags, "-shared", src, "-o", out + ".tmp", *ldflags]
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError(f"torch ops build failed:\n{res.stderr[-6000:]}")
+    os.replace(out + ".tmp", out)
+    if verbose:
+        print(f"[eks_amd.build] linked {out}")
+    return out
 
 
 def _deps() -> list[str]:
@@ -67,7 +111,8 @@ def _compile(src: str, obj: str) -> None:
 
 def build(force: bool = False, jobs: int | None = None, verbose: bool = True) -> str:
     os.makedirs(OBJDIR, exist_ok=True)
-    srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
+    srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")) +
+                  [c for c in glob.glob(os.path.join(CSRC, "*.cpp")) if not c.endswith(TORCH_SRC)])
     deps = _deps()
     todo = []
     objs = []
@@ -92,6 +137,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = True) ->
         os.replace(lib + ".tmp", lib)
         if verbose:
             print(f"[eks_amd.build] linked {lib}")
+    build_torch_ops(force=force, verbose=verbose)
     return lib
 
 
