@@ -24,13 +24,16 @@
 //                 interpolation -> threshold, and the kept-frame bit mask
 //   k_fit_accum   one lane per (trajectory, chunk): ensemble again (or the y
 //                 hand-off plane + the frame mask), keep frames with
-//                 v_t <= threshold, chunk statistics of y and of
-//                 the differences between consecutive kept frames (shifted
-//                 sums -> mean / scatter matrix), first / last kept y
-//   k_fit_final   one lane per trajectory: merge the chunks in order (Chan
-//                 et al. pairwise update; the kept-frame pair straddling
-//                 two chunks is added here), PCA by cyclic Jacobi on the
-//                 n x n scatter matrix, parameter rows
+//                 v_t <= threshold, chunk sums of y - K and its outer
+//                 products (K = the trajectory's frame-0 ensemble, a shift
+//                 that keeps the one-pass sums well conditioned), of the
+//                 differences between consecutive kept frames and their
+//                 outer products, first / last kept y
+//   k_fit_merge   sums of the chunk partials in order (plain additions; the
+//                 kept-frame pair straddling two chunks added where they meet)
+//   k_fit_final   one wave per trajectory: means / scatter matrices from the
+//                 sums, PCA by cyclic Jacobi on the n x n scatter matrix,
+//                 parameter rows
 // The results agree with the numpy fit to rounding (different summation
 // order), which moves the smoothed outputs by ~1e-12 px.
 #include <hip/hip_runtime.h>
@@ -96,13 +99,20 @@ struct FitShape {
   long long Lc;    // frames per chunk
 };
 
+// the shift K of trajectory b (its frame-0 ensemble y, n values), written by
+// k_fit_accum's chunk-0 lanes for k_fit_final
+struct FitShift {
+  double *K;
+};
+
 constexpr int kTile = 16;  // frames per register tile: one 128-byte row segment per lane
 
 template <int E, int N, typename T, typename YT>
 __global__ __launch_bounds__(256) void k_fit_worst(const T *__restrict__ obs, FitShape sh,
                                                    long long sb, long long st, long long se,
                                                    long long sj, int Ert, int median,
-                                                   double *__restrict__ worst, YevOut yo) {
+                                                   double *__restrict__ worst, YevOut yo,
+                                                   FitShift ks) {
   // each lane computes kTile consecutive frames of its (trajectory, chunk)
   // into LDS; the block then writes the trajectory-major rows as whole
   // 128-byte segments (16 lanes per segment) instead of one 8-byte store
@@ -127,6 +137,9 @@ __global__ __launch_bounds__(256) void k_fit_worst(const T *__restrict__ obs, Fi
         double y[N], ev[N];
         frame_ensemble<E, N, T>(pb + (t + k) * st, se, sj, Ert, median != 0, y, ev,
                                 tile[threadIdx.x][k]);
+        if (t + k == 0)  // the trajectory's shift for the accumulation (frame 0's ensemble)
+#pragma unroll
+          for (int j = 0; j < N; ++j) ks.K[b * N + j] = y[j];
         if (yo.y)
 #pragma unroll
           for (int j = 0; j < N; ++j) {
@@ -142,6 +155,9 @@ __global__ __launch_bounds__(256) void k_fit_worst(const T *__restrict__ obs, Fi
           double y[N], ev[N], v;
           frame_ensemble<E, N, T>(pb + u * st, se, sj, Ert, median != 0, y, ev, v);
           worst[b * sh.T + u] = v;
+          if (u == 0)
+#pragma unroll
+            for (int j = 0; j < N; ++j) ks.K[b * N + j] = y[j];
           if (yo.y)
 #pragma unroll
             for (int j = 0; j < N; ++j) {
@@ -464,11 +480,214 @@ __global__ __launch_bounds__(BLK) void k_fit_select(const double *__restrict__ w
   }
 }
 
-// per-chunk statistics, packed symmetric matrices (upper triangle, row-major)
+// ---------------------------------------------------------------------------
+// The same selection for FEW long rows (B < kSelSplitB trajectories): one
+// block per row leaves most of the chip idle (config 2: 17 blocks), so each
+// row is cut into segments of kSegKeys keys, one block per (row, segment),
+// in four launches:
+//   k_sel_hist   top-digit histogram of the segment in LDS, added to the
+//                row's global histogram (no-return atomics), NaN flag
+//   k_sel_bin    one block per row: the bin of rank lo (scan of the global
+//                histogram), zeroes the row's candidate counter
+//   k_sel_cand   per segment: kept-frame mask words of the frames below the
+//                bin (ballot), the bin's keys and frame indices appended to
+//                the row's candidate buffer (wave-aggregated slots; their
+//                order varies, the order statistics do not), the least key
+//                above the bin (atomicMin)
+//   k_sel_final  one block per row: MSD radix select of ranks lo / lo + 1
+//                among the candidates (LDS when they fit, else in place),
+//                numpy's _lerp, the bin's kept frames marked in the mask
+// Same threshold and mask bits as k_fit_select (tests/test_gpu_fit_mask.py).
+// ---------------------------------------------------------------------------
+constexpr long long kSelSplitB = 512;
+}  // namespace
+// eks_debug_set(EKS_DBG_FIT_SELECT): 0 automatic, 1 one block per row, 2 split
+long long g_fit_select = 0;
+namespace {
+constexpr long long kSegKeys = 1024;
+
+struct SelRow {  // per-row state of the split selection (zeroed by a memset)
+  unsigned nan, ncand;
+  unsigned long long binpfx, kin, cnt_bin, above;  // above: least key above the bin
+};
+
+__global__ __launch_bounds__(256) void k_sel_hist(const double *__restrict__ worst, long long TT,
+                                                  int G, unsigned *__restrict__ ghist,
+                                                  SelRow *__restrict__ rows) {
+  __shared__ unsigned hist[kBins];
+  constexpr int lo_bit = 51;
+  const long long b = blockIdx.x / G, g = blockIdx.x % G;
+  const uint64_t *keys = reinterpret_cast<const uint64_t *>(worst + b * TT);
+  const long long k0 = g * kSegKeys, k1 = k0 + kSegKeys < TT ? k0 + kSegKeys : TT;
+  for (int i = threadIdx.x; i < kBins; i += 256) hist[i] = 0;
+  __syncthreads();
+  bool nan = false;
+  for (long long i = k0 + threadIdx.x; i < k1; i += 256) {
+    const uint64_t x = keys[i];
+    nan |= (x & 0x7fffffffffffffffull) > 0x7ff0000000000000ull;
+    atomicAdd(&hist[(unsigned)(x >> lo_bit) & (kBins - 1)], 1u);
+  }
+  if (__any(nan) && (threadIdx.x & 63) == 0) atomicOr(&rows[b].nan, 1u);
+  __syncthreads();
+  unsigned *gh = ghist + b * kBins;
+  for (int i = threadIdx.x; i < kBins; i += 256)
+    if (hist[i]) atomicAdd(&gh[i], hist[i]);
+}
+
+__global__ __launch_bounds__(256) void k_sel_bin(const unsigned *__restrict__ ghist, long long lo,
+                                                 SelRow *__restrict__ rows) {
+  __shared__ long long si[2 + 4];
+  const long long b = blockIdx.x;
+  const unsigned *h = ghist + b * kBins;
+  constexpr unsigned per = kBins / 256;
+  long long mine = 0;
+  for (unsigned d = threadIdx.x * per; d < (threadIdx.x + 1) * per; ++d) mine += h[d];
+  long long total;
+  long long acc = block_excl_scan<256>(mine, si + 2, total);
+  if (lo >= acc && lo < acc + mine) {  // exactly one thread
+    unsigned d = threadIdx.x * per;
+    while (acc + h[d] <= (unsigned long long)lo) acc += h[d++];
+    rows[b].binpfx = (unsigned long long)d << 51;
+    rows[b].kin = lo - acc;
+    rows[b].cnt_bin = h[d];
+  }
+  if (threadIdx.x == 0) {
+    rows[b].ncand = 0;
+    rows[b].above = ~0ull;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_sel_cand(const double *__restrict__ worst, long long TT,
+                                                  int G, SelRow *__restrict__ rows,
+                                                  uint64_t *__restrict__ ckey,
+                                                  unsigned *__restrict__ cidx,
+                                                  uint64_t *__restrict__ kept, long long W) {
+  const long long b = blockIdx.x / G, g = blockIdx.x % G;
+  const uint64_t *keys = reinterpret_cast<const uint64_t *>(worst + b * TT);
+  const long long k0 = g * kSegKeys, k1 = k0 + kSegKeys < TT ? k0 + kSegKeys : TT;
+  SelRow &row = rows[b];
+  const bool nan = row.nan != 0;
+  const uint64_t binpfx = row.binpfx, binmask = ~((1ull << 51) - 1);
+  uint64_t *krow = kept ? kept + b * W : nullptr;
+  uint64_t *ck = ckey + b * TT;
+  unsigned *ci = cidx + b * TT;
+  unsigned long long above = ~0ull;
+  // whole waves per 64-key word: k0 is a multiple of 64 and every wave of the
+  // loop runs the same iterations (the index test is on the wave's last lane)
+  for (long long i0 = k0 + (threadIdx.x & ~63); i0 < k1; i0 += 256) {
+    const long long i = i0 + (threadIdx.x & 63);
+    const bool in_row = i < k1;
+    const uint64_t x = in_row ? keys[i] : ~0ull;
+    if (krow) {
+      const uint64_t mb = __ballot(in_row && !nan && x < binpfx);  // below the bin: kept
+      if ((threadIdx.x & 63) == 0) krow[i0 >> 6] = mb;
+    }
+    if (nan) continue;
+    const bool in = in_row && (x & binmask) == binpfx;
+    if (in_row && (x & binmask) > binpfx && x < above) above = x;
+    const uint64_t m = __ballot(in);
+    if (m == 0) continue;
+    const int lane = threadIdx.x & 63;
+    const unsigned below = (unsigned)__popcll(m & ((1ull << lane) - 1));
+    unsigned base = 0;
+    if (lane == __ffsll((long long)m) - 1) base = atomicAdd(&row.ncand, (unsigned)__popcll(m));
+    base = __shfl(base, __ffsll((long long)m) - 1, 64);
+    if (in) {
+      ck[base + below] = x;
+      ci[base + below] = (unsigned)i;
+    }
+  }
+  if (!nan && above != ~0ull) atomicMin(&row.above, above);
+}
+
+template <int BLK>
+__global__ __launch_bounds__(BLK) void k_sel_final(const double *__restrict__ worst, long long TT,
+                                                   long long hi_minus_lo, double g,
+                                                   const SelRow *__restrict__ rows,
+                                                   const uint64_t *__restrict__ ckey,
+                                                   const unsigned *__restrict__ cidx,
+                                                   double *__restrict__ thr,
+                                                   uint64_t *__restrict__ kept, long long W) {
+  __shared__ unsigned hsel[1 << kSelDigit];
+  __shared__ uint64_t cand[kCand];
+  __shared__ uint64_t su[4];
+  __shared__ long long si[2 + BLK / 64];
+  const long long b = blockIdx.x;
+  const SelRow row = rows[b];
+  uint64_t *krow = kept ? kept + b * W : nullptr;
+  if (row.nan) {  // np.percentile of an array holding NaN is NaN: no frame kept
+    if (threadIdx.x == 0) thr[b] = __builtin_nan("");
+    return;  // (k_sel_cand wrote zero mask words)
+  }
+  const uint64_t binpfx = row.binpfx;
+  const long long kin = (long long)row.kin, cnt = (long long)row.cnt_bin;
+  const uint64_t *ck = ckey + b * TT;
+  const unsigned *ci = cidx + b * TT;
+  constexpr int lo_bit = 51;
+  uint64_t ka;
+  const uint64_t *src = ck;
+  if (cnt <= kCand) {
+    for (long long i = threadIdx.x; i < cnt; i += BLK) cand[i] = ck[i];
+    __syncthreads();
+    src = cand;
+  }
+  ka = block_select<BLK, kSelDigit>(src, cnt, kin, lo_bit - 1, binpfx, hsel, su, si);
+  uint64_t kb = ka;
+  if (hi_minus_lo) {
+    // rank lo + 1: ka again if it repeats in the bin, else the next key of the
+    // bin, else the least key above the bin
+    if (threadIdx.x == 0) {
+      su[1] = ~0ull;
+      si[0] = 0;
+    }
+    __syncthreads();
+    unsigned long long c = 0, ab = ~0ull;
+    for (long long i = threadIdx.x; i < cnt; i += BLK) {
+      const uint64_t x = src[i];
+      c += x <= ka;
+      if (x > ka && x < ab) ab = x;
+    }
+    atomicAdd((unsigned long long *)&si[0], c);
+    atomicMin((unsigned long long *)&su[1], ab);
+    __syncthreads();
+    const long long le = si[0];
+    const unsigned long long nxt = su[1];
+    kb = le >= kin + 2 ? ka : nxt != ~0ull ? nxt : row.above;
+  }
+  __shared__ double sthr;
+  if (threadIdx.x == 0) {
+    const double a = __longlong_as_double((long long)ka);
+    const double bb = __longlong_as_double((long long)kb);
+    const double d = bb - a;  // numpy's _lerp
+    const double t = g >= 0.5 ? bb - d * (1.0 - g) : a + d * g;
+    thr[b] = t;
+    sthr = t;
+  }
+  if (!krow) return;
+  __syncthreads();
+  const double th = sthr;
+  // the bin's kept frames; keys above the bin are >= kb >= th: kept only
+  // when equal to th, i.e. th == kb with kb above the bin (then the keys
+  // equal to kb, all outside the candidates, are marked from the row)
+  for (long long i = threadIdx.x; i < cnt; i += BLK)
+    if (__longlong_as_double((long long)src[i]) <= th)
+      atomicOr((unsigned long long *)&krow[ci[i] >> 6], 1ull << (ci[i] & 63));
+  const bool amb = (kb & ~((1ull << lo_bit) - 1)) != binpfx &&
+                   th >= __longlong_as_double((long long)kb);
+  if (amb) {
+    const uint64_t *keys = reinterpret_cast<const uint64_t *>(worst + b * TT);
+    for (long long i = threadIdx.x; i < TT; i += BLK)
+      if (keys[i] == kb) atomicOr((unsigned long long *)&krow[i >> 6], 1ull << (i & 63));
+  }
+}
+
+// per-chunk statistics, packed symmetric matrices (upper triangle, row-major):
+// kept-frame count, sum of z = y - K and of z z^T, kept-pair count, sum of
+// the pair differences d and of d d^T, first / last kept y
 template <int N>
 struct ChunkStats {
   static constexpr int kTri = N * (N + 1) / 2;
-  // [cnt | mean N | M2 tri | npair | dmean N | dM2 tri | first N | last N]
+  // [cnt | S1 N | S2 tri | npair | D1 N | D2 tri | first N | last N]
   static constexpr int cnt = 0, mean = 1, M = 1 + N;
   static constexpr int npair = 1 + N + kTri, dmean = npair + 1, dM = dmean + N;
   static constexpr int first = dM + kTri, last = first + N;
@@ -480,28 +699,108 @@ EKS_DEV constexpr int tri(int i, int j) {  // i <= j
   return i * N - i * (i - 1) / 2 + (j - i);
 }
 
-template <int E, int N, typename T, typename YT, bool FROM_YEV>
+// the sums of a frame range, merged as  L (+) R  (R the later frames)
+template <int N>
+struct Partial {
+  static constexpr int kTri = N * (N + 1) / 2;
+  double cnt, S1[N], S2[kTri], np, D1[N], D2[kTri], first[N], last[N];
+  EKS_DEV void merge_right(const Partial &R) {
+    if (R.cnt == 0.0) return;
+    if (cnt == 0.0) {
+      *this = R;
+      return;
+    }
+    // the kept pair where the ranges meet, then the right range's own sums
+    // (k_fit_merge adds in the same order)
+    double d[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) d[i] = R.first[i] - last[i];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      D1[i] += d[i];
+#pragma unroll
+      for (int j = i; j < N; ++j) D2[tri<N>(i, j)] = fma(d[i], d[j], D2[tri<N>(i, j)]);
+    }
+    np += 1.0;
+    cnt += R.cnt;
+#pragma unroll
+    for (int i = 0; i < N; ++i) S1[i] += R.S1[i];
+#pragma unroll
+    for (int i = 0; i < kTri; ++i) S2[i] += R.S2[i];
+    np += R.np;
+#pragma unroll
+    for (int i = 0; i < N; ++i) D1[i] += R.D1[i];
+#pragma unroll
+    for (int i = 0; i < kTri; ++i) D2[i] += R.D2[i];
+#pragma unroll
+    for (int i = 0; i < N; ++i) last[i] = R.last[i];
+  }
+  EKS_DEV Partial shfl_down(int delta) const {
+    Partial o;
+    auto mv = [&](double x) { return __shfl_down(x, delta, 64); };
+    o.cnt = mv(cnt);
+    o.np = mv(np);
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      o.S1[i] = mv(S1[i]);
+      o.D1[i] = mv(D1[i]);
+      o.first[i] = mv(first[i]);
+      o.last[i] = mv(last[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < kTri; ++i) {
+      o.S2[i] = mv(S2[i]);
+      o.D2[i] = mv(D2[i]);
+    }
+    return o;
+  }
+};
+
+// Lane mappings: trajectory-fastest (many trajectories: coalesced plane
+// loads, a few chunks per trajectory) or, with WAVE_MERGE (few long
+// trajectories), 64 consecutive chunks of one trajectory per wave, whose
+// partials the wave merges by a shuffle tree into one (fixed order): the
+// merge kernel then sees T / (64 Lc) partials per trajectory instead of
+// T / Lc.
+template <int E, int N, typename T, typename YT, bool FROM_YEV, bool WAVE_MERGE>
 __global__ __launch_bounds__(256) void k_fit_accum(const T *__restrict__ obs, FitShape sh,
                                                    long long sb, long long st, long long se,
                                                    long long sj, int Ert, int median,
                                                    const double *__restrict__ thr,
                                                    const uint64_t *__restrict__ kept,
                                                    long long W, double *__restrict__ part,
-                                                   YevOut yi) {
+                                                   YevOut yi, FitShift ks) {
   using CS = ChunkStats<N>;
   const long long lane = blockIdx.x * (long long)blockDim.x + threadIdx.x;
-  if (lane >= sh.B * sh.NC) return;
-  const long long b = lane % sh.B, c = lane / sh.B;
-  const long long t0 = c * sh.Lc, t1 = t0 + sh.Lc < sh.T ? t0 + sh.Lc : sh.T;
+  const long long NCp = WAVE_MERGE ? (sh.NC + 63) / 64 * 64 : sh.NC;  // chunks per trajectory, padded
+  if (!WAVE_MERGE && lane >= sh.B * sh.NC) return;
+  if (WAVE_MERGE && lane >= sh.B * NCp) return;  // (whole waves: NCp is a multiple of 64)
+  const long long b = WAVE_MERGE ? lane / NCp : lane % sh.B;
+  const long long c = WAVE_MERGE ? lane % NCp : lane / sh.B;
+  const long long t0 = c * sh.Lc < sh.T ? c * sh.Lc : sh.T;
+  const long long t1 = t0 + sh.Lc < sh.T ? t0 + sh.Lc : sh.T;
   const T *pb = obs + b * sb;
   const double th = thr[b];
   const uint64_t *krow = FROM_YEV ? kept + b * W : nullptr;
-  uint64_t kw = FROM_YEV ? krow[t0 >> 6] : 0ull;
-  // shifted sums: y relative to the chunk's first kept frame K
-  double K[N], S1[N], S2[CS::kTri], D1[N], D2[CS::kTri], last[N];
+  auto y_of = [&](long long t, double (&y)[N]) {
+    if constexpr (FROM_YEV) {
+#pragma unroll
+      for (int j = 0; j < N; ++j) y[j] = (double)((const YT *)yi.y)[(t * N + j) * sh.B + b];
+    } else {
+      double v;
+      frame_ensemble<E, N, T>(pb + t * st, se, sj, Ert, median != 0, y, v);
+    }
+  };
+  // the trajectory's shift: its frame-0 ensemble, written by k_fit_worst (a
+  // NaN there means a NaN variance, hence a NaN threshold: no kept frame)
+  double K[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j) K[j] = ks.K[b * N + j];
+  uint64_t kw = (FROM_YEV && t0 < t1) ? krow[t0 >> 6] : 0ull;
+  double S1[N], S2[CS::kTri], D1[N], D2[CS::kTri], first[N], last[N];
   double cnt = 0.0, npair = 0.0;
 #pragma unroll
-  for (int i = 0; i < N; ++i) K[i] = S1[i] = D1[i] = last[i] = 0.0;
+  for (int i = 0; i < N; ++i) S1[i] = D1[i] = first[i] = last[i] = 0.0;
 #pragma unroll
   for (int i = 0; i < CS::kTri; ++i) S2[i] = D2[i] = 0.0;
   for (long long t = t0; t < t1; ++t) {
@@ -512,8 +811,7 @@ __global__ __launch_bounds__(256) void k_fit_accum(const T *__restrict__ obs, Fi
       // reading the ev plane took)
       if ((t & 63) == 0) kw = krow[t >> 6];
       if (!((kw >> (t & 63)) & 1ull)) continue;
-#pragma unroll
-      for (int j = 0; j < N; ++j) y[j] = (double)((const YT *)yi.y)[(t * N + j) * sh.B + b];
+      y_of(t, y);
     } else {
       double v;
       frame_ensemble<E, N, T>(pb + t * st, se, sj, Ert, median != 0, y, v);
@@ -521,7 +819,7 @@ __global__ __launch_bounds__(256) void k_fit_accum(const T *__restrict__ obs, Fi
     }
     if (cnt == 0.0) {
 #pragma unroll
-      for (int i = 0; i < N; ++i) K[i] = y[i];
+      for (int i = 0; i < N; ++i) first[i] = y[i];
     } else {
       double d[N];
 #pragma unroll
@@ -548,30 +846,57 @@ __global__ __launch_bounds__(256) void k_fit_accum(const T *__restrict__ obs, Fi
     }
     cnt += 1.0;
   }
-  double *o = part + lane * (long long)CS::kLen;
-  const double ic = cnt > 0.0 ? 1.0 / cnt : 0.0;
-  const double ip = npair > 0.0 ? 1.0 / npair : 0.0;
-  o[CS::cnt] = cnt;
-  o[CS::npair] = npair;
+  Partial<N> pt;
+  pt.cnt = cnt;
+  pt.np = npair;
 #pragma unroll
   for (int i = 0; i < N; ++i) {
-    o[CS::mean + i] = K[i] + S1[i] * ic;
-    o[CS::dmean + i] = D1[i] * ip;
-    o[CS::first + i] = K[i];
-    o[CS::last + i] = last[i];
+    pt.S1[i] = S1[i];
+    pt.D1[i] = D1[i];
+    pt.first[i] = first[i];
+    pt.last[i] = last[i];
+  }
+#pragma unroll
+  for (int i = 0; i < CS::kTri; ++i) {
+    pt.S2[i] = S2[i];
+    pt.D2[i] = D2[i];
+  }
+  long long slot = lane;  // partial row: (chunk, trajectory) -> c * B + b
+  if constexpr (WAVE_MERGE) {
+    // tree over the wave's 64 chunks: lane l merges lane l + 2^k at level k
+#pragma unroll
+    for (int k = 1; k < 64; k <<= 1) {
+      const Partial<N> r = pt.shfl_down(k);
+      if ((threadIdx.x & (2 * k - 1)) == 0) pt.merge_right(r);
+    }
+    if ((threadIdx.x & 63) != 0) return;
+    slot = (c / 64) * sh.B + b;
+  }
+  double *o = part + slot * (long long)CS::kLen;
+  o[CS::cnt] = pt.cnt;
+  o[CS::npair] = pt.np;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    o[CS::mean + i] = pt.S1[i];
+    o[CS::dmean + i] = pt.D1[i];
+    o[CS::first + i] = pt.first[i];
+    o[CS::last + i] = pt.last[i];
 #pragma unroll
     for (int j = i; j < N; ++j) {
-      o[CS::M + tri<N>(i, j)] = S2[tri<N>(i, j)] - S1[i] * S1[j] * ic;
-      o[CS::dM + tri<N>(i, j)] = D2[tri<N>(i, j)] - D1[i] * D1[j] * ip;
+      o[CS::M + tri<N>(i, j)] = pt.S2[tri<N>(i, j)];
+      o[CS::dM + tri<N>(i, j)] = pt.D2[tri<N>(i, j)];
     }
   }
 }
 
-// Merge F consecutive chunk partials of one trajectory into one, in order
-// (Chan, Golub & LeVeque pairwise update; the kept pair straddling two
-// chunks is added as a one-sample difference).  One thread per (trajectory,
-// group, packed matrix element); every thread recomputes the counts and the
-// means it needs, so there is no cross-thread dependence.
+// Merge F consecutive chunk partials of one trajectory into one, in order:
+// the sums add, and where two non-empty ranges meet the kept pair straddling
+// them (first kept y of the right minus last kept y of the left) adds one
+// difference.  One thread per (trajectory, group, packed matrix element);
+// every thread reads the counts and the first / last values it needs, so
+// there is no cross-thread dependence.  The F partials' loads are issued
+// kMergeUnroll at a time ahead of the (sequential, fixed-order) additions.
+constexpr int kMergeUnroll = 4;
 template <int N>
 __global__ __launch_bounds__(256) void k_fit_merge(long long B, int nc_in, int F,
                                                    const double *__restrict__ in,
@@ -587,52 +912,57 @@ __global__ __launch_bounds__(256) void k_fit_merge(long long B, int nc_in, int F
   int i = 0;
   while (tri<N>(i, N - 1) < e) ++i;  // element e = (i, j), i <= j
   const int j = i + (e - tri<N>(i, i));
-  double n = 0.0, mi = 0.0, mj = 0.0, Mij = 0.0;
-  double np_ = 0.0, di = 0.0, dj = 0.0, Dij = 0.0;
-  double fi = 0.0, fj = 0.0, li = 0.0, lj = 0.0;
+  double n = 0.0, si = 0.0, s2 = 0.0, np_ = 0.0, di = 0.0, dj = 0.0, d2 = 0.0;
+  double fi = 0.0, li = 0.0, lj = 0.0;
   bool have = false;
   const int c0 = (int)g * F, c1 = c0 + F < nc_in ? c0 + F : nc_in;
-  for (int c = c0; c < c1; ++c) {
-    const double *o = in + ((long long)c * B + b) * CS::kLen;
-    const double cnt = o[CS::cnt];
-    if (cnt == 0.0) continue;
-    if (have) {  // pair (last kept of the previous chunks, first kept of this one)
-      const double xi = o[CS::first + i] - li, xj = o[CS::first + j] - lj;
-      const double nn = np_ + 1.0, f = np_ / nn;
-      Dij += (xi - di) * (xj - dj) * f;
-      di += (xi - di) / nn;
-      dj += (xj - dj) / nn;
-      np_ = nn;
-    } else {
-      fi = o[CS::first + i];
-      fj = o[CS::first + j];
+  for (int cb = c0; cb < c1; cb += kMergeUnroll) {
+    double v[kMergeUnroll][11];
+#pragma unroll
+    for (int u = 0; u < kMergeUnroll; ++u) {
+      const int c = cb + u < c1 ? cb + u : c1 - 1;  // clamped: a re-read, not used
+      const double *o = in + ((long long)c * B + b) * CS::kLen;
+      v[u][0] = o[CS::cnt];
+      v[u][1] = o[CS::first + i];
+      v[u][2] = o[CS::first + j];
+      v[u][3] = o[CS::mean + i];
+      v[u][4] = o[CS::M + e];
+      v[u][5] = o[CS::npair];
+      v[u][6] = o[CS::dmean + i];
+      v[u][7] = o[CS::dmean + j];
+      v[u][8] = o[CS::dM + e];
+      v[u][9] = o[CS::last + i];
+      v[u][10] = o[CS::last + j];
     }
-    {
-      const double nb = cnt, nn = n + nb, f = n * nb / nn;
-      const double dli = o[CS::mean + i] - mi, dlj = o[CS::mean + j] - mj;
-      Mij += o[CS::M + e] + dli * dlj * f;
-      mi += dli * (nb / nn);
-      mj += dlj * (nb / nn);
-      n = nn;
+#pragma unroll
+    for (int u = 0; u < kMergeUnroll; ++u) {
+      if (cb + u >= c1 || v[u][0] == 0.0) continue;
+      if (have) {  // the pair (last kept of the ranges before, first kept of this one)
+        const double xi = v[u][1] - li, xj = v[u][2] - lj;
+        di += xi;
+        dj += xj;
+        d2 = fma(xi, xj, d2);
+        np_ += 1.0;
+      } else {
+        fi = v[u][1];
+      }
+      n += v[u][0];
+      si += v[u][3];
+      s2 += v[u][4];
+      np_ += v[u][5];
+      di += v[u][6];
+      dj += v[u][7];
+      d2 += v[u][8];
+      li = v[u][9];
+      lj = v[u][10];
+      have = true;
     }
-    const double npb = o[CS::npair];
-    if (npb > 0.0) {
-      const double nn = np_ + npb, f = np_ * npb / nn;
-      const double dli = o[CS::dmean + i] - di, dlj = o[CS::dmean + j] - dj;
-      Dij += o[CS::dM + e] + dli * dlj * f;
-      di += dli * (npb / nn);
-      dj += dlj * (npb / nn);
-      np_ = nn;
-    }
-    li = o[CS::last + i];
-    lj = o[CS::last + j];
-    have = true;
   }
   double *w = out + ((long long)g * B + b) * CS::kLen;
-  w[CS::M + e] = Mij;
-  w[CS::dM + e] = Dij;
+  w[CS::M + e] = s2;
+  w[CS::dM + e] = d2;
   if (i == j) {
-    w[CS::mean + i] = mi;
+    w[CS::mean + i] = si;
     w[CS::dmean + i] = di;
     w[CS::first + i] = fi;
     w[CS::last + i] = li;
@@ -650,7 +980,7 @@ __global__ __launch_bounds__(256) void k_fit_merge(long long B, int nc_in, int F
 // broadcasts and two lane shuffles, no matrix leaves the registers.
 template <int R, int N>
 __global__ __launch_bounds__(64) void k_fit_final(long long B, const double *__restrict__ part,
-                                                  int kind, double smooth_param,
+                                                  FitShift ks, int kind, double smooth_param,
                                                   double *__restrict__ params,
                                                   int32_t *__restrict__ status) {
   using CS = ChunkStats<N>;
@@ -664,13 +994,18 @@ __global__ __launch_bounds__(64) void k_fit_final(long long B, const double *__r
   double np_ = o[CS::npair];
   if (np_ < 1.0) np_ = __builtin_nan("");  // np.cov of no pairs is NaN
   const int ti = own ? (i <= j ? tri<N>(i, j) : tri<N>(j, i)) : 0;
-  const double Mij = own ? o[CS::M + ti] : 0.0;   // good-frame scatter matrix
-  const double Dij = own ? o[CS::dM + ti] : 0.0;  // difference scatter matrix
+  // centred scatter matrices from the shifted sums: sum z z^T - S1 S1^T / n
+  // (good frames; z = y - K) and sum d d^T - D1 D1^T / np (kept-pair
+  // differences)
+  const double s1i = own ? o[CS::mean + i] : 0.0, s1j = own ? o[CS::mean + j] : 0.0;
+  const double d1i = own ? o[CS::dmean + i] : 0.0, d1j = own ? o[CS::dmean + j] : 0.0;
+  const double Mij = own ? o[CS::M + ti] - s1i * (s1j / n) : 0.0;
+  const double Dij = own ? o[CS::dM + ti] - d1i * (d1j / np_) : 0.0;
   ParamLayout<R, N> P;
   double *pr = params + b * (long long)P.len;
   if (L < R) pr[P.m0 + L] = 0.0;
   if (L < R * R) pr[P.A + L] = (L / R == L % R) ? 1.0 : 0.0;
-  if (L < N) pr[P.off + L] = o[CS::mean + L];
+  if (L < N) pr[P.off + L] = ks.K[b * N + L] + o[CS::mean + L] / n;  // mean of the good y
   if (kind == EKS_FIT_SINGLEVIEW) {
     // S0 = diag(var(good y)) (ddof 0), Q = s cov(diff) (ddof 1), A = C = I
     if (own && i < R && j < R) {
@@ -682,6 +1017,13 @@ __global__ __launch_bounds__(64) void k_fit_final(long long B, const double *__r
     // principal axes of the good-frame scatter matrix (sklearn's PCA axes
     // up to sign; outputs do not depend on the sign)
     double a = Mij, v = (own && i == j) ? 1.0 : 0.0;
+    // parallel cyclic Jacobi (round-robin ordering): each sweep is N - 1
+    // rounds of N / 2 disjoint rotations, applied at once as A <- J^T A J,
+    // V <- V J (lane (i, j) combines the entries of its row pair x column
+    // pair: four reads, no dependence on the other rotations of the round)
+    const int Nm = N - 1;
+    auto slot_of = [&](int x, int k) { return x == 0 ? 0 : 1 + (x - 1 + Nm - (k % Nm)) % Nm; };
+    auto idx_at = [&](int pos, int k) { return pos == 0 ? 0 : 1 + (pos - 1 + k) % Nm; };
     for (int sweep = 0; sweep < 60; ++sweep) {
       double off = (own && i < j) ? a * a : 0.0, dia = (own && i == j) ? a * a : 0.0;
 #pragma unroll
@@ -690,32 +1032,42 @@ __global__ __launch_bounds__(64) void k_fit_final(long long B, const double *__r
         dia += __shfl_xor(dia, w, 64);
       }
       if (off == 0.0 || off <= 1e-34 * dia) break;
-      for (int p = 0; p < N - 1; ++p)
-        for (int q = p + 1; q < N; ++q) {
+      for (int k = 0; k < Nm; ++k) {
+        // the partner of index x in round k: positions pos and N-1-pos pair up
+        auto partner = [&](int x) { return idx_at(Nm - slot_of(x, k), k); };
+        const int pi = partner(i), pj = partner(j);
+        // rotation of the pair {x, partner}: J_pp = c, J_pq = s, J_qp = -s,
+        // J_qq = c with p < q; returns (J_xx, J_partner,x)
+        auto rot = [&](int x, int px, double &jxx, double &jpx) {
+          const int p = x < px ? x : px, q = x < px ? px : x;
           const double apq = __shfl(a, p * N + q, 64);
-          if (apq == 0.0) continue;  // wave-uniform
           const double app = __shfl(a, p * N + p, 64), aqq = __shfl(a, q * N + q, 64);
-          const double theta = (aqq - app) / (2.0 * apq);
-          const double t = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
-          const double c = 1.0 / sqrt(t * t + 1.0), sn = t * c;
-          // columns p, q:  a_ip' = c a_ip - s a_iq ; a_iq' = s a_ip + c a_iq  (same for V)
-          const int cp = (j == p) ? i * N + q : (j == q) ? i * N + p : L;
-          const double ao = __shfl(a, cp, 64), vo = __shfl(v, cp, 64);
-          if (own && j == p) {
-            a = c * a - sn * ao;
-            v = c * v - sn * vo;
-          } else if (own && j == q) {
-            a = sn * ao + c * a;
-            v = sn * vo + c * v;
+          double c = 1.0, sn = 0.0;
+          if (apq != 0.0) {
+            const double theta = (aqq - app) / (2.0 * apq);
+            const double t = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+            c = 1.0 / sqrt(t * t + 1.0);
+            sn = t * c;
           }
-          // rows p, q:  a_pj'' = c a_pj' - s a_qj' ; a_qj'' = s a_pj' + c a_qj'
-          const int rp = (i == p) ? q * N + j : (i == q) ? p * N + j : L;
-          const double ar = __shfl(a, rp, 64);
-          if (own && i == p)
-            a = c * a - sn * ar;
-          else if (own && i == q)
-            a = sn * ar + c * a;
+          jxx = c;
+          jpx = x == p ? -sn : sn;  // J_qp = -s (x = p), J_pq = s (x = q)
+        };
+        double ji, jpi_i, jj, jpj_j;
+        rot(own ? i : 0, own ? pi : partner(0), ji, jpi_i);
+        rot(own ? j : 0, own ? pj : partner(0), jj, jpj_j);
+        const int li = own ? i : 0, lj = own ? j : 0, lpi = own ? pi : 0, lpj = own ? pj : 0;
+        const double a_ipj = __shfl(a, li * N + lpj, 64);
+        const double a_pij = __shfl(a, lpi * N + lj, 64);
+        const double a_pipj = __shfl(a, lpi * N + lpj, 64);
+        const double v_ipj = __shfl(v, li * N + lpj, 64);
+        if (own) {
+          // A'_ij = sum_{k in {i, pi}, l in {j, pj}} J_ki A_kl J_lj
+          const double r0 = a * jj + a_ipj * jpj_j;       // (A J)_ij
+          const double r1 = a_pij * jj + a_pipj * jpj_j;  // (A J)_{pi j}
+          a = ji * r0 + jpi_i * r1;
+          v = v * jj + v_ipj * jpj_j;
         }
+      }
     }
     if (own) {
       sV[L] = v;
@@ -764,11 +1116,12 @@ __global__ __launch_bounds__(64) void k_fit_final(long long B, const double *__r
   if (status && L == 0) status[b] = n > 0.0 ? 0 : EKS_STATUS_SINGULAR;
 }
 
-// chunks per trajectory: enough lanes to fill the chip (~256k), chunks of
-// >= 64 frames, a multiple of kTile frames each
+// chunks per trajectory (k_fit_worst's and k_fit_accum's lanes): enough
+// lanes to fill the chip (~256k), chunks of >= kTile frames, a multiple of
+// kTile frames each
 void fit_chunks(long long B, long long T, int &nc, long long &lc) {
   long long n = (262144 + B - 1) / (B > 0 ? B : 1);
-  const long long cap = T / 64 > 1 ? T / 64 : 1;
+  const long long cap = T / kTile > 1 ? T / kTile : 1;
   if (n > cap) n = cap;
   if (n < 1) n = 1;
   lc = (T + n - 1) / n;
@@ -777,6 +1130,10 @@ void fit_chunks(long long B, long long T, int &nc, long long &lc) {
 }
 
 constexpr int kMergeFan = 16;
+
+// few long trajectories: k_fit_accum merges each wave's 64 chunks itself
+bool fit_wave_merge(int nc) { return nc >= 64; }
+int fit_partials(int nc) { return fit_wave_merge(nc) ? (nc + 63) / 64 : nc; }
 
 }  // namespace
 
@@ -790,10 +1147,15 @@ extern "C" size_t eks_fit_workspace_bytes(int64_t B, int64_t T, int n) {
   long long lc;
   fit_chunks(B, T, nc, lc);
   const long long len = 2 + 4LL * n + (long long)n * (n + 1);
-  const long long nc2 = (nc + kMergeFan - 1) / kMergeFan;
+  const long long np = fit_partials(nc);
+  const long long nc2 = (np + kMergeFan - 1) / kMergeFan;
   const long long W = (T + 63) / 64;  // frame-mask words per trajectory
-  // worst plane, thresholds, chunk partials, kept-frame mask
-  return (size_t)(B * T + B + B * (nc + nc2) * len + B * W) * sizeof(double);
+  // worst plane, thresholds, chunk partials, kept-frame mask, shifts K
+  size_t bytes = (size_t)(B * T + B + B * (np + nc2) * len + B * W + B * n) * sizeof(double);
+  // split selection: histograms, row states, candidate keys + indices
+  if (B < kSelSplitB || g_fit_select == 2)
+    bytes += (size_t)B * kBins * 4 + (size_t)B * sizeof(SelRow) + (size_t)B * T * 12 + 256;
+  return bytes;
 }
 
 // y of the hand-off planes is float32 exactly when it is a member value:
@@ -842,11 +1204,23 @@ extern "C" int eks_fit(const void *obs, int obs_dtype, int64_t B, int64_t T, int
   const long long len = 2 + 4LL * n + (long long)n * (n + 1);
   double *worst = (double *)workspace;
   double *thr = worst + B * T;
+  const int npart = fit_partials(sh.NC);
+  const bool wave_merge = fit_wave_merge(sh.NC);
   double *partA = thr + B;
-  double *partB = partA + B * (long long)sh.NC * len;
+  double *partB = partA + B * (long long)npart * len;
   const long long W = (T + 63) / 64;
   uint64_t *kept = reinterpret_cast<uint64_t *>(
-      partB + B * (long long)((sh.NC + kMergeFan - 1) / kMergeFan) * len);
+      partB + B * (long long)((npart + kMergeFan - 1) / kMergeFan) * len);
+  FitShift ks{reinterpret_cast<double *>(kept + B * W)};
+  // split selection (few rows): its buffers after the shifts
+  const bool split_sel = g_fit_select == 1 ? false : g_fit_select == 2 ? true : B < kSelSplitB;
+  const int G = (int)((T + kSegKeys - 1) / kSegKeys);
+  char *sel_base = reinterpret_cast<char *>(ks.K + B * n);
+  unsigned *ghist = reinterpret_cast<unsigned *>(sel_base);
+  SelRow *rows = reinterpret_cast<SelRow *>(sel_base + (size_t)B * kBins * 4);
+  uint64_t *ckey = reinterpret_cast<uint64_t *>(
+      (reinterpret_cast<uintptr_t>(rows + B) + 255) / 256 * 256);
+  unsigned *cidx = reinterpret_cast<unsigned *>(ckey + B * T);
   // np.percentile 'linear': virtual index (T - 1) q / 100
   const double vi = (double)(T - 1) * (quantile_keep / 100.0);
   const long long lo = (long long)floor(vi);
@@ -882,35 +1256,54 @@ extern "C" int eks_fit(const void *obs, int obs_dtype, int64_t B, int64_t T, int
         prof_call_begin();
         prof_mark(s, "k_fit_worst");
         hipLaunchKernelGGL((k_fit_worst<EE, NN, Tp, YT>), dim3(grid), dim3(256), 0, s,
-                           (const Tp *)obs, sh, sb, st, se, sj, E, median, worst, yo);
+                           (const Tp *)obs, sh, sb, st, se, sj, E, median, worst, yo, ks);
         int rc = check_launch("k_fit_worst");
         if (rc) return rc;
         prof_mark(s, "k_fit_select");
         // with the hand-off planes written, the selection also writes the
         // kept-frame mask k_fit_accum reads instead of the ev plane
-        if (T >= 65536)
+        if (split_sel) {
+          // few long rows: one block per (row, segment) in four launches
+          if (hipMemsetAsync(ghist, 0, (size_t)B * kBins * 4 + (size_t)B * sizeof(SelRow), s) !=
+              hipSuccess)
+            return set_err(EKS_ERR_HIP, "eks_fit: hipMemsetAsync failed");
+          const unsigned gs = (unsigned)(B * G);
+          hipLaunchKernelGGL(k_sel_hist, dim3(gs), dim3(256), 0, s, worst, T, G, ghist, rows);
+          hipLaunchKernelGGL(k_sel_bin, dim3((unsigned)B), dim3(256), 0, s, ghist, lo, rows);
+          hipLaunchKernelGGL(k_sel_cand, dim3(gs), dim3(256), 0, s, worst, T, G, rows, ckey, cidx,
+                             yev ? kept : nullptr, W);
+          hipLaunchKernelGGL(k_sel_final<256>, dim3((unsigned)B), dim3(256), 0, s, worst, T, hi - lo,
+                             g, rows, ckey, cidx, thr, yev ? kept : nullptr, W);
+        } else if (T >= 65536) {
           hipLaunchKernelGGL(k_fit_select<1024>, dim3((unsigned)B), dim3(1024), 0, s, worst, T,
                              lo, hi, g, thr, yev ? kept : nullptr, W);
-        else
+        } else {
           hipLaunchKernelGGL(k_fit_select<256>, dim3((unsigned)B), dim3(256), 0, s, worst, T, lo,
                              hi, g, thr, yev ? kept : nullptr, W);
+        }
         if ((rc = check_launch("k_fit_select"))) return rc;
         prof_mark(s, "k_fit_accum");
         // with the hand-off planes written, the second pass reads the y plane
         // and the frame mask (8 B per frame for n = 2 with float32 y) instead
         // of the members (40 B) and skips the sort
-        if (yev)
-          hipLaunchKernelGGL((k_fit_accum<EE, NN, Tp, YT, true>), dim3(grid), dim3(256), 0, s,
-                             (const Tp *)obs, sh, sb, st, se, sj, E, median, thr, kept, W, partA,
-                             yo);
-        else
-          hipLaunchKernelGGL((k_fit_accum<EE, NN, Tp, YT, false>), dim3(grid), dim3(256), 0, s,
-                             (const Tp *)obs, sh, sb, st, se, sj, E, median, thr, kept, W, partA,
-                             yo);
+        auto accum = [&](auto from_yev, auto wm) {
+          constexpr bool FY = decltype(from_yev)::value != 0, WM = decltype(wm)::value != 0;
+          const long long lanes = WM ? B * (long long)npart * 64 : B * (long long)sh.NC;
+          hipLaunchKernelGGL((k_fit_accum<EE, NN, Tp, YT, FY, WM>), dim3(grid_for(lanes, 256)),
+                             dim3(256), 0, s, (const Tp *)obs, sh, sb, st, se, sj, E, median, thr,
+                             kept, W, partA, yo, ks);
+        };
+        if (yev) {
+          if (wave_merge) accum(ic<1>{}, ic<1>{});
+          else accum(ic<1>{}, ic<0>{});
+        } else {
+          if (wave_merge) accum(ic<0>{}, ic<1>{});
+          else accum(ic<0>{}, ic<0>{});
+        }
         if ((rc = check_launch("k_fit_accum"))) return rc;
         // merge the chunk partials in order, kMergeFan at a time, ping-pong
         double *src = partA, *dst = partB;
-        int nc = sh.NC;
+        int nc = npart;
         while (nc > 1) {
           const int nout = (nc + kMergeFan - 1) / kMergeFan;
           const long long threads = B * (long long)nout * ChunkStats<NN>::kTri;
@@ -930,7 +1323,7 @@ extern "C" int eks_fit(const void *obs, int obs_dtype, int64_t B, int64_t T, int
             return set_err(EKS_ERR_ARG, "eks_fit: r > n");
           } else {
             hipLaunchKernelGGL((k_fit_final<RR, NN>), dim3((unsigned)B), dim3(64), 0, s, B, src,
-                               kind, smooth_param, params, status);
+                               ks, kind, smooth_param, params, status);
             return check_launch("k_fit_final");
           }
         });

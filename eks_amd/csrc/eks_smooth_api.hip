@@ -42,6 +42,7 @@ namespace eks {
 int launch_rt(const SmoothArgs &a);
 long long g_wait_ticks = kDefaultWaitTicks;
 long long g_a3_slice_bytes = 0;
+extern long long g_fit_select;  // eks_fit.hip
 }
 
 extern "C" {
@@ -187,6 +188,11 @@ int64_t eks_debug_set(int key, int64_t value) {
     case EKS_DBG_A3_SLICE_BYTES: {
       const long long prev = g_a3_slice_bytes;
       g_a3_slice_bytes = value > 0 ? value : 0;
+      return prev;
+    }
+    case EKS_DBG_FIT_SELECT: {
+      const long long prev = g_fit_select;
+      g_fit_select = value == 1 || value == 2 ? value : 0;
       return prev;
     }
     default: return set_err(EKS_ERR_ARG, "eks_debug_set: unknown key %d", key), -1;

@@ -321,8 +321,13 @@ int eks_interp1d(const double *x, int64_t nx, const double *y, int64_t ncol, int
  *   EKS_DBG_A3_SLICE_BYTES largest member byte offset span of one algo-3
  *                          launch (0 = 4 GB, the buffer descriptor's range);
  *                          a smaller span forces the batch slicing.
+ *   EKS_DBG_FIT_SELECT     eks_fit's percentile selection: 0 = automatic
+ *                          (split over row segments for B < 512 rows), 1 =
+ *                          one block per row, 2 = split (both must give the
+ *                          same threshold and kept-frame mask).  The
+ *                          workspace size follows the setting.
  */
-enum { EKS_DBG_WAIT_US = 1, EKS_DBG_A3_SLICE_BYTES = 2 };
+enum { EKS_DBG_WAIT_US = 1, EKS_DBG_A3_SLICE_BYTES = 2, EKS_DBG_FIT_SELECT = 3 };
 int64_t eks_debug_set(int key, int64_t value);
 
 /*

@@ -31,14 +31,26 @@ def torch():
 
 
 def _fit_both(torch, st, q, n=2, r=2, kind="singleview"):
-    from eks_amd import batch
+    """The member path and the mask path, each with both selection kernels
+    (one block per row, and the split over row segments that few rows use):
+    all four parameter sets bit-identical."""
+    from eks_amd import _lib, batch
     obs = torch.from_numpy(np.ascontiguousarray(st)).cuda().permute(0, 2, 1, 3)  # (B,T,E,n)
     kw = dict(kind=kind, n=n, r=r, smooth_param=0.01, quantile_keep=q, check=False)
-    p0, s0 = batch.fit(obs, **kw)
-    p1, s1, _ = batch.fit(obs, keep_yev=True, **kw)
-    p0, p1 = p0.cpu().numpy(), p1.cpu().numpy()
-    np.testing.assert_array_equal(s0.cpu().numpy(), s1.cpu().numpy())
-    assert np.array_equal(p0, p1, equal_nan=True), np.nanmax(np.abs(p0 - p1))
+    res = []
+    prev = _lib.debug_set(_lib.EKS_DBG_FIT_SELECT, 1)
+    try:
+        for sel in (1, 2):
+            _lib.debug_set(_lib.EKS_DBG_FIT_SELECT, sel)
+            p0, s0 = batch.fit(obs, **kw)
+            p1, s1, _ = batch.fit(obs, keep_yev=True, **kw)
+            res += [(p0.cpu().numpy(), s0.cpu().numpy()), (p1.cpu().numpy(), s1.cpu().numpy())]
+    finally:
+        _lib.debug_set(_lib.EKS_DBG_FIT_SELECT, prev)
+    p1 = res[1][0]
+    for k, (p, st_) in enumerate(res):
+        np.testing.assert_array_equal(st_, res[0][1])
+        assert np.array_equal(p, p1, equal_nan=True), (k, np.nanmax(np.abs(p - p1)))
     return p1
 
 
