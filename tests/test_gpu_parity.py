@@ -200,6 +200,39 @@ def test_fused_singleview_golden(torch, path, dtype):
     _close(res["ms"][0].cpu().numpy(), g["ms"], rtol=1e-8)
 
 
+@pytest.mark.parametrize("name", ["quant3", "quant5"])
+def test_quantised_members_keep_reference_frames(torch, name):
+    """Members on a 0.25 px grid (E = 3 and 5): the worst variances tie in
+    large groups, so the percentile threshold equals many frames' values.
+    The device ensemble (mean and variance scaled by 1/E and 1/E^2, within
+    1-2 ulp of numpy's / E: ensemble.hpp) and the device fit (eks_fit, both
+    selection paths) must keep exactly the frames the reference keeps
+    (``good`` in the fixture, eks/multiview_pca_smoother.py:685-688's rule
+    applied by tools/gen_golden.py with the reference's ensemble): the
+    offsets are means over the kept frames, so one frame more or less moves
+    them by ~1e-3 relative."""
+    from eks_amd import _lib, batch
+    g = np.load(os.path.join(GOLDEN, f"singleview_{name}.npz"))
+    obs = g["obs"]  # (E, T, 2), float32-exact
+    d = batch.make_time_major(obs[None], dtype=np.float32)
+    import eks_amd.ops  # noqa: F401
+    # the ensemble variances: equal to the reference's to 2 ulp
+    _, ev = torch.ops.eks.ensemble(d, "median")
+    np.testing.assert_allclose(ev[0].cpu().numpy(), g["ev"], rtol=4.5e-16, atol=0)
+    for sel in (1, 2):
+        prev = _lib.debug_set(_lib.EKS_DBG_FIT_SELECT, sel)
+        try:
+            params, st = batch.fit(d, kind="singleview", n=2, r=2, smooth_param=float(g["s"]),
+                                   quantile_keep=float(g["q"]))
+        finally:
+            _lib.debug_set(_lib.EKS_DBG_FIT_SELECT, prev)
+        p = params[0].cpu().numpy()
+        off = p[-2:]
+        np.testing.assert_allclose(off, g["means"], rtol=1e-12, atol=0)
+        np.testing.assert_allclose(p[2:6].reshape(2, 2), g["S0"], rtol=1e-10, atol=1e-12)
+        np.testing.assert_allclose(p[10:14].reshape(2, 2), g["Q"], rtol=1e-9, atol=1e-14)
+
+
 def _oracle_smooth_batch(stacks, models, O):
     outs = []
     for st, m in zip(stacks, models):
