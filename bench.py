@@ -79,6 +79,10 @@ def parse():
                          "all_gathers of per-segment aggregates) instead of replicas")
     ap.add_argument("--no-graph", action="store_true",
                     help="launch every step eagerly instead of replaying a captured HIP graph")
+    ap.add_argument("--a3-mode", type=int, default=0,
+                    help="tuning: algo 3's launch form (eks_debug_set EKS_DBG_A3_MODE: 0 default, "
+                         "1 two launches, 2 one launch, v >= 3 one launch in batches of v - 2 "
+                         "groups)")
     ap.add_argument("--scaling", choices=["strong", "weak"], default="strong",
                     help="config 4: strong = the video batch is split over ranks; weak = "
                          "every rank smooths --videos videos")
@@ -607,6 +611,8 @@ def main():
     dev = torch.device("cuda", local)
     _lib.require_gpu()
     t_setup = time.perf_counter()
+    if a.a3_mode:
+        _lib.debug_set(_lib.EKS_DBG_A3_MODE, a.a3_mode)
     if a.config in (2, 4):
         w = workload_singleview(torch, a, dev, rank, world, a.config)
     elif a.config == 3:

@@ -76,6 +76,9 @@ struct Plan3 {
   // sync block (zeroed every call): ticket counters (own 128-byte lines),
   // then one flag word per unit for each pass
   size_t sync_bytes = 0, flag1_off = 0, flag2_off = 0;
+  // one launch for both passes (k3_fused): per k3_fwd unit, "its fine start
+  // states are stored" (the bwd units that read them wait for it)
+  size_t flag3_off = 0;
   size_t fst_off = 0, inc2_off = 0, nllp_off = 0, prm_off = 0, total = 0;
   // look-back aggregates: k3_fwd's unit elements, k3_bwd's 4 chunk maps per unit
   size_t agg1_off = 0, agg2_off = 0;
@@ -93,7 +96,8 @@ inline Plan3 make_plan3(long long B, long long T, int r, int n) {
   p.units_f = p.NCu * p.ng;
   p.flag1_off = 256;
   p.flag2_off = p.flag1_off + (size_t)p.units_f * 4;
-  p.sync_bytes = align256(p.flag2_off + (size_t)p.units * 4);
+  p.flag3_off = p.flag2_off + (size_t)p.units * 4;
+  p.sync_bytes = align256(p.flag3_off + (size_t)p.units_f * 4);
   size_t off = p.sync_bytes;
   auto take = [&](size_t bytes) {
     const size_t o = off;
@@ -127,16 +131,16 @@ inline Plan3 make_plan3(long long B, long long T, int r, int n) {
 EKS_DEV __amdgpu_buffer_rsrc_t member_rsrc(const void *p) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, -1, 0x00020000);
 }
-template <typename T>
+template <typename T, bool NT>
 EKS_DEV T member_load(__amdgpu_buffer_rsrc_t rs, unsigned voff, int soff) {
-  constexpr int aux = kNtLoad ? 2 : 0;  // nt: streamed once
+  constexpr int aux = NT ? 2 : 0;  // nt: streamed once
   if constexpr (sizeof(T) == 4)
     return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(rs, voff, soff, aux));
   else
     return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, aux));
 }
 
-template <int E, int N, typename T, int D>
+template <int E, int N, typename T, int D, bool NT = kNtLoad>
 struct MemberRing {
   T v[D][E][N];
   const char *base;  // uniform
@@ -163,7 +167,7 @@ struct MemberRing {
 #pragma unroll
     for (int e = 0; e < E; ++e)
 #pragma unroll
-      for (int j = 0; j < N; ++j) v[slot][e][j] = member_load<T>(rs, loff, e * seb + j * sjb);
+      for (int j = 0; j < N; ++j) v[slot][e][j] = member_load<T, NT>(rs, loff, e * seb + j * sjb);
   }
   EKS_DEV void get(int slot, double (&avg)[N], double (&rv)[N]) const {
 #pragma unroll
@@ -177,7 +181,7 @@ struct MemberRing {
 };
 
 // the ensemble handed over as y / ev planes (EKS_YEV32 / EKS_YEV64 inputs)
-template <int N, typename YT, int D>
+template <int N, typename YT, int D, bool NT = kNtLoad>
 struct YevRing {
   YT y[D][N];
   double ev[D][N];
@@ -195,7 +199,7 @@ struct YevRing {
   EKS_DEV void fetch(int slot, long long t) {
 #pragma unroll
     for (int j = 0; j < N; ++j) {
-      if constexpr (kNtLoad) {
+      if constexpr (NT) {
         y[slot][j] = __builtin_nontemporal_load(&pl(yb, t * N + j, B, b));
         ev[slot][j] = __builtin_nontemporal_load(&pl(eb, t * N + j, B, b));
       } else {
@@ -213,13 +217,13 @@ struct YevRing {
   }
 };
 
-template <int E, int N, typename T, int D>
+template <int E, int N, typename T, int D, bool NT = kNtLoad>
 struct SrcOf {
-  using type = MemberRing<E, N, T, D>;
+  using type = MemberRing<E, N, T, D, NT>;
 };
-template <int E, int N, typename YT, int D>
-struct SrcOf<E, N, YevIn<YT>, D> {
-  using type = YevRing<N, YT, D>;
+template <int E, int N, typename YT, int D, bool NT>
+struct SrcOf<E, N, YevIn<YT>, D, NT> {
+  using type = YevRing<N, YT, D, NT>;
 };
 
 // Look-back payloads in time-major planes, stored write-through / loaded
@@ -348,6 +352,87 @@ unsigned persistent_grid(long long units) {
 }
 
 // ---------------------------------------------------------------------------
+// Ticket schedules.  Separate launches (mode 0: k3_fwd, mode 1: k3_bwd): a
+// ticket is a unit, time-chunk major.  One launch for both passes (mode 2,
+// k3_fused): the tickets run F_0, F_1, B_0, F_2, B_1, ..., F_{NB-1},
+// B_{NB-2}, B_{NB-1} over batches of GB 64-trajectory groups, F_k = the
+// k3_fwd units of batch k (time-chunk major) and B_k = its k3_bwd units
+// (reverse time).  Every unit waits only for units with smaller tickets:
+// its chain neighbours, and (B_k) the F_k units that stored its fine start
+// states.  GB = ng: all forward units, then all backward ones (the backward
+// pass starts where the forward one ends, its first units re-reading the
+// members the last forward units just read); small GB: the backward pass of
+// a batch follows its forward pass one batch later, so its member re-read
+// comes (in part) from the Infinity Cache.
+// ---------------------------------------------------------------------------
+struct Sched3 {
+  int mode = 0;  // 0 fwd only, 1 bwd only, 2 both
+  long long ng = 0, GB = 0, NB = 0, gl = 0, NCu = 0, NCc = 0;
+};
+struct Work3 {
+  int phase;  // 0 a k3_fwd unit, 1 a k3_bwd unit, 2 none (the grid drains)
+  long long c, grp;  // time chunk (k3_bwd: counted from the end), group
+};
+inline Sched3 make_sched3(const Plan3 &p, int mode, long long gb) {
+  Sched3 s;
+  s.mode = mode;
+  s.ng = p.ng;
+  s.GB = gb > 0 && gb < p.ng ? gb : p.ng;
+  s.NB = (p.ng + s.GB - 1) / s.GB;
+  s.gl = p.ng - (s.NB - 1) * s.GB;
+  s.NCu = p.NCu;
+  s.NCc = p.NCc;
+  return s;
+}
+EKS_DEV Work3 decode3(const Sched3 &s, unsigned long long t) {
+  Work3 w{2, 0, 0};
+  const long long tt = (long long)t;
+  if (s.mode != 2) {
+    const long long nc = s.mode == 0 ? s.NCu : s.NCc;
+    if (tt < nc * s.ng) {
+      w.phase = s.mode;
+      w.c = tt / s.ng;
+      w.grp = tt - w.c * s.ng;
+    }
+    return w;
+  }
+  auto seg = [&](int ph, long long batch, long long l) {
+    const long long gk = batch == s.NB - 1 ? s.gl : s.GB;
+    w.phase = ph;
+    w.c = l / gk;
+    w.grp = batch * s.GB + (l - w.c * gk);
+  };
+  const long long g0 = s.NB == 1 ? s.gl : s.GB;
+  if (tt < s.NCu * g0) {
+    seg(0, 0, tt);
+    return w;
+  }
+  long long r = tt - s.NCu * g0;
+  const long long P = (s.NCu + s.NCc) * s.GB;  // pair k (1 <= k <= NB-2): F_k, B_{k-1}
+  if (s.NB >= 3 && r < (s.NB - 2) * P) {
+    const long long k = 1 + r / P, q = r - (k - 1) * P;
+    if (q < s.NCu * s.GB) seg(0, k, q);
+    else seg(1, k - 1, q - s.NCu * s.GB);
+    return w;
+  }
+  if (s.NB >= 2) {
+    r -= (s.NB - 2) * P;
+    if (r < s.NCu * s.gl) {
+      seg(0, s.NB - 1, r);
+      return w;
+    }
+    r -= s.NCu * s.gl;
+    if (r < s.NCc * s.GB) {
+      seg(1, s.NB - 2, r);
+      return w;
+    }
+    r -= s.NCc * s.GB;
+  }
+  if (r < s.NCc * s.gl) seg(1, s.NB - 1, r);
+  return w;
+}
+
+// ---------------------------------------------------------------------------
 // k3_fwd: filtering elements + the forward chain (filtered states).  A unit
 // is KPU = 4 x FPW fine chunks: each wave streams FPW consecutive ones (two
 // at r = 2: 128-step units, half the chain links and half the per-unit tail
@@ -356,32 +441,48 @@ unsigned persistent_grid(long long units) {
 template <int R>
 constexpr int fwd_fpw() { return R <= 2 ? 2 : 1; }
 
-template <int R, int N, int E, typename T, int AI, int CI>
-__global__ __launch_bounds__(64 * kWV) void k3_fwd(SmoothArgs a, Plan3 p) {
+// LDS of one k3_fwd unit (doubles): each wave's first element (FPW = 2), each
+// wave's element then the prefix compositions, the state entering the unit
+template <int R>
+constexpr int fwd_lds_doubles() {
+  return ((fwd_fpw<R>() > 1 ? kWV : 1) + kWV) * Elem<R>::len * 64 + (R + Sym<R>::len) * 64;
+}
+// k3_fused's forward member loads: default cache policy, so that the
+// backward units of the same batch find the members in the Infinity Cache
+constexpr bool kFusedFwdNt = false;
+
+// The k3_fwd units of consecutive tickets from t on (a run ends at the
+// first ticket that is not a k3_fwd unit, which is returned).  FUSED: the
+// fine start states are stored write-through and each unit sets its
+// flag3 word once they are (k3_fused's backward units wait for it).
+template <int R, int N, int E, typename T, int AI, int CI, bool FUSED>
+EKS_DEV unsigned k3_fwd_run(const SmoothArgs &a, const Plan3 &p, const Sched3 &sc, unsigned t,
+                            double *lds, unsigned *tk, unsigned *ctr, int &it) {
   constexpr int EL = Elem<R>::len, KS = R + Sym<R>::len;
   constexpr int D = kK3D;
   constexpr int LF = fine_len3(R, N);
   constexpr int FPW = fwd_fpw<R>(), KPU = kWV * FPW;
-  __shared__ double shA[FPW > 1 ? kWV : 1][EL][64];  // each wave's first element (FPW = 2)
-  __shared__ double shX[kWV][EL][64];  // each wave's element, then prefix compositions
-  __shared__ double shS[KS][64];       // filtered state entering the unit
-  __shared__ unsigned tk[2];
+  constexpr int NA = FPW > 1 ? kWV : 1;
+  auto &shA = *reinterpret_cast<double (*)[NA][EL][64]>(lds);  // each wave's first element (FPW = 2)
+  auto &shX = *reinterpret_cast<double (*)[kWV][EL][64]>(lds + NA * EL * 64);  // each wave's element, then prefixes
+  auto &shS = *reinterpret_cast<double (*)[KS][64]>(lds + (NA + kWV) * EL * 64);  // state entering the unit
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63;
   const long long B = a.B, TT = a.T;
-  unsigned *ctr = (unsigned *)a.ws;
   unsigned *flags = (unsigned *)(a.ws + p.flag1_off);
+  unsigned *done = (unsigned *)(a.ws + p.flag3_off);
   double *fst = (double *)(a.ws + p.fst_off);
   double *agg1 = (double *)(a.ws + p.agg1_off);
   const double *prm = (const double *)(a.ws + p.prm_off);
-  typename SrcOf<E, N, T, D>::type src;  // member ring, persists across units
+  // member ring, persists across the units of the run
+  typename SrcOf<E, N, T, D, FUSED ? kFusedFwdNt : kNtLoad>::type src;
   src.init(a);
   Model<R, N> md;
-  // model + the first member steps of unit tt (structure checked by
+  // model + the first member steps of unit wk (structure checked by
   // k_model_planes).  Lanes past the last trajectory read trajectory 0 (their
   // results are never stored): every branch here is wave-uniform.
-  auto head = [&](unsigned tt) {
-    if (tt >= (unsigned long long)p.units_f) return;
-    const long long c = tt / p.ng, g = tt - c * p.ng, ff = (c * kWV + w) * FPW;
+  auto head = [&](const Work3 &wk) {
+    if (wk.phase != 0) return;
+    const long long c = wk.c, g = wk.grp, ff = (c * kWV + w) * FPW;
     const unsigned bb = (unsigned)(g * 64 + l);
     const unsigned bl = (long long)bb < B ? bb : 0u;
     if (ff < p.NCf) {
@@ -400,14 +501,12 @@ __global__ __launch_bounds__(64 * kWV) void k3_fwd(SmoothArgs a, Plan3 p) {
 #pragma unroll
       for (int j = i; j < R; ++j) P[i][j] = P[j][i] = shS[k++][l];
   };
-  if (threadIdx.x == 0) tk[0] = atomicAdd(ctr, 1u);
-  __syncthreads();
-  unsigned t = __builtin_amdgcn_readfirstlane(tk[0]);  // uniform: every index below in SGPRs
-  head(t);
-  for (int it = 0; t < (unsigned long long)p.units_f; ++it) {
+  Work3 wk = decode3(sc, t);  // uniform: every index below in SGPRs
+  head(wk);
+  while (wk.phase == 0) {
     unsigned tnext = 0;
     if (threadIdx.x == 0) tnext = atomicAdd(ctr, 1u);  // consumed after the streaming
-    const long long cu = t / p.ng, grp = t - cu * p.ng;
+    const long long cu = wk.c, grp = wk.grp;
     const long long f0 = (cu * kWV + w) * FPW;  // the wave's first fine chunk
     const unsigned b = (unsigned)(grp * 64 + l);
     const bool lane_ok = (long long)b < B;
@@ -491,10 +590,11 @@ __global__ __launch_bounds__(64 * kWV) void k3_fwd(SmoothArgs a, Plan3 p) {
     if (threadIdx.x == 0) tk[(it + 1) & 1] = tnext;
     __syncthreads();
     const unsigned tn = __builtin_amdgcn_readfirstlane(tk[(it + 1) & 1]);
+    const Work3 wn = decode3(sc, tn);
     // the next unit's first member steps in flight during this unit's tail
     // (wave 0 after its chain wait: vmcnt counts in order, so a prefetch
     // issued before the poll would hold the poll back until it lands)
-    if (w != 0) head(tn);
+    if (w != 0) head(wn);
     // prefix over the waves (dead chunks / lanes hold the identity, which
     // composes exactly): round 1 X01 -> slot 1, X23 -> slot 3
     if (w == 1 || w == 3) {
@@ -547,10 +647,18 @@ __global__ __launch_bounds__(64 * kWV) void k3_fwd(SmoothArgs a, Plan3 p) {
         }
         if (lane_ok) {
           state_load_pl_wt<R>(fst, ((j + 1) * KPU) * KS, B, b, m, P);
-          for (long long i = j + 1; i < cu; ++i) {
+          // fold the elements of units j+1 .. cu-1, the next one's loads in
+          // flight while one is composed (a walk back over many units is then
+          // ~one L2 / MALL latency per element, not a load round trip each)
+          if (j + 1 < cu) {
             Elem<R> Ei;
-            elem_load_pl_wt<R>(Ei, agg1, i * EL, B, b);
-            ok = compose_state<R>(m, P, Ei) && ok;
+            elem_load_pl_wt<R>(Ei, agg1, (j + 1) * EL, B, b);
+            for (long long i = j + 1; i < cu; ++i) {
+              Elem<R> En;
+              if (i + 1 < cu) elem_load_pl_wt<R>(En, agg1, (i + 1) * EL, B, b);
+              ok = compose_state<R>(m, P, Ei) && ok;
+              Ei = En;
+            }
           }
         }
       }
@@ -568,7 +676,7 @@ __global__ __launch_bounds__(64 * kWV) void k3_fwd(SmoothArgs a, Plan3 p) {
         if (lane_ok) state_store_pl_wt<R>(fst, ((cu + 1) * KPU) * KS, B, b, m, P);
         publish_flag(flags + cu * p.ng + grp, l, kIncReady);
       }
-      head(tn);
+      head(wn);
     }
     __syncthreads();
     // fine start states: wave w's first chunk starts from the entering state
@@ -582,53 +690,87 @@ __global__ __launch_bounds__(64 * kWV) void k3_fwd(SmoothArgs a, Plan3 p) {
         Elem<R> Ep;
         Ep.load(&shX[w - 1][0][l], 64);
         ok = compose_state<R>(m, P, Ep) && ok;
-        store_state_pl<R>(fst, f0 * KS, B, b, m, P);
+        if constexpr (FUSED) state_store_pl_wt<R>(fst, f0 * KS, B, b, m, P);
+        else store_state_pl<R>(fst, f0 * KS, B, b, m, P);
       }
       if constexpr (FPW > 1) {
         if (f0 + 1 < p.NCf) {
           Elem<R> Ea;
           Ea.load(&shA[w][0][l], 64);
           ok = compose_state<R>(m, P, Ea) && ok;
-          store_state_pl<R>(fst, (f0 + 1) * KS, B, b, m, P);
+          if constexpr (FUSED) state_store_pl_wt<R>(fst, (f0 + 1) * KS, B, b, m, P);
+          else store_state_pl<R>(fst, (f0 + 1) * KS, B, b, m, P);
         }
       }
     }
     if (lane_ok)
       flag(a.status, b, (ok ? 0 : EKS_STATUS_SCAN) | (okf ? 0 : EKS_STATUS_SINGULAR));
+    // FUSED: every wave's fine-start stores drained before the barrier, then
+    // one flag for the unit (the next unit's prefetch, if issued, is waited
+    // for too: vmcnt counts loads and stores in order)
+    if constexpr (FUSED) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();  // LDS free for the next unit
+    if constexpr (FUSED)
+      if (threadIdx.x == 0)
+        __hip_atomic_store((k3_gu32 *)(done + cu * p.ng + grp), 1u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
     t = tn;
+    wk = wn;
+    ++it;
   }
+  return t;
+}
+
+template <int R, int N, int E, typename T, int AI, int CI>
+__global__ __launch_bounds__(64 * kWV) void k3_fwd(SmoothArgs a, Plan3 p, Sched3 sc) {
+  __shared__ double lds[fwd_lds_doubles<R>()];
+  __shared__ unsigned tk[2];
+  unsigned *ctr = (unsigned *)a.ws;
+  if (threadIdx.x == 0) tk[0] = atomicAdd(ctr, 1u);
+  __syncthreads();
+  int it = 0;
+  k3_fwd_run<R, N, E, T, AI, CI, false>(a, p, sc, __builtin_amdgcn_readfirstlane(tk[0]), lds, tk,
+                                        ctr, it);
 }
 
 // ---------------------------------------------------------------------------
 // k3_bwd: the final smoothing pass + the backward chain (smoothed means)
 // ---------------------------------------------------------------------------
-template <int R, int N, int E, typename T, int AI, int CI, bool NLL>
-__global__ __launch_bounds__(64 * kWV) void k3_bwd(SmoothArgs a, Plan3 p) {
+// LDS of one k3_bwd unit (doubles): the filtered states of the first NL
+// steps of every lane, the RTS maps of waves 1..3 (then their entering means)
+template <int R, int N>
+constexpr int bwd_lds_doubles() {
+  return lds_steps3(R, N) * (R + Sym<R>::len) * 64 * kWV + (kWV - 1) * (R * R + R) * 64;
+}
+
+// The k3_bwd units of consecutive tickets from t on (a run ends at the first
+// ticket that is not a k3_bwd unit, which is returned).  FUSED: each wave
+// first waits for the k3_fwd unit that stored its fine chunk's start state.
+template <int R, int N, int E, typename T, int AI, int CI, bool NLL, bool FUSED>
+EKS_DEV unsigned k3_bwd_run(const SmoothArgs &a, const Plan3 &p, const Sched3 &sc, unsigned t,
+                            double *lds, unsigned *tk, unsigned *ctr, int &it) {
   constexpr int KS = R + Sym<R>::len, MP = R * R + R;
   constexpr int D = kK3D;
   constexpr int NR = reg_steps3(R, N), NL = lds_steps3(R, N), LF = NR + NL;
-  __shared__ double fs[NL][KS][64 * kWV];  // filtered states of the first NL steps
-  __shared__ double shM[kWV - 1][MP][64];  // RTS maps of waves 1..3, then their entering means
-  __shared__ unsigned tk[2];
+  constexpr int KPUF = kWV * fwd_fpw<R>();  // fine chunks per k3_fwd unit
+  auto &fs = *reinterpret_cast<double (*)[NL][KS][64 * kWV]>(lds);  // filtered states, first NL steps
+  auto &shM = *reinterpret_cast<double (*)[kWV - 1][MP][64]>(lds + NL * KS * 64 * kWV);  // maps of waves 1..3
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63;
   const int tid = threadIdx.x;
   const long long B = a.B, TT = a.T;
-  unsigned *ctr = (unsigned *)a.ws + 32;
   unsigned *flags = (unsigned *)(a.ws + p.flag2_off);
+  const unsigned *done = (const unsigned *)(a.ws + p.flag3_off);
   const double *fst = (const double *)(a.ws + p.fst_off);
   double *inc = (double *)(a.ws + p.inc2_off);
   double *agg2 = (double *)(a.ws + p.agg2_off);
   const double *prm = (const double *)(a.ws + p.prm_off);
   const bool vec2 = N == 2 && a.oj == 1 && ((a.ob | a.ot) & 1) == 0 &&
                     (((uintptr_t)a.out) & 15) == 0;
-  if (tid == 0) tk[0] = atomicAdd(ctr, 1u);
-  __syncthreads();
-  unsigned t = __builtin_amdgcn_readfirstlane(tk[0]);  // uniform: every index below in SGPRs
-  for (int it = 0; t < (unsigned long long)p.units; ++it) {
+  Work3 wk = decode3(sc, t);  // uniform: every index below in SGPRs
+  while (wk.phase == 1) {
     unsigned tnext = 0;
     if (tid == 0) tnext = atomicAdd(ctr, 1u);
-    const long long cr = t / p.ng, grp = t - cr * p.ng;
+    const long long cr = wk.c, grp = wk.grp;
     const long long cc = p.NCc - 1 - cr;  // units in reverse time order
     const long long f = cc * kWV + w;
     const unsigned b = (unsigned)(grp * 64 + l);
@@ -646,6 +788,10 @@ __global__ __launch_bounds__(64 * kWV) void k3_bwd(SmoothArgs a, Plan3 p) {
     // 0's data and store nothing
     const unsigned bl = lane_ok ? b : 0u;
     if (f < p.NCf) {
+      // FUSED: the start state of fine chunk f was stored by k3_fwd unit
+      // (f - 1) / KPUF of this group (an earlier ticket)
+      if constexpr (FUSED)
+        if (f >= 1 && !wait_flag(done + ((f - 1) / KPUF) * p.ng + grp, a.wait_ticks)) okc = false;
       load_model_pl<R, N, AI, CI>(prm, B, bl, f == 0, md);
       double m[R], P[R][R];
       if (f == 0) {
@@ -655,6 +801,8 @@ __global__ __launch_bounds__(64 * kWV) void k3_bwd(SmoothArgs a, Plan3 p) {
 #pragma unroll
           for (int j = 0; j < R; ++j) P[i][j] = md.S0[i][j];
         }
+      } else if constexpr (FUSED) {
+        state_load_pl_wt<R>(fst, f * KS, B, bl, m, P);
       } else {
         load_state_pl<R>(fst, f * KS, B, bl, m, P);
       }
@@ -924,6 +1072,45 @@ __global__ __launch_bounds__(64 * kWV) void k3_bwd(SmoothArgs a, Plan3 p) {
     if (tid == 0) tk[(it + 1) & 1] = tnext;
     __syncthreads();  // LDS free for the next unit, its ticket visible
     t = __builtin_amdgcn_readfirstlane(tk[(it + 1) & 1]);
+    wk = decode3(sc, t);
+    ++it;
+  }
+  return t;
+}
+
+template <int R, int N, int E, typename T, int AI, int CI, bool NLL>
+__global__ __launch_bounds__(64 * kWV) void k3_bwd(SmoothArgs a, Plan3 p, Sched3 sc) {
+  __shared__ double lds[bwd_lds_doubles<R, N>()];
+  __shared__ unsigned tk[2];
+  unsigned *ctr = (unsigned *)a.ws + 32;
+  if (threadIdx.x == 0) tk[0] = atomicAdd(ctr, 1u);
+  __syncthreads();
+  int it = 0;
+  k3_bwd_run<R, N, E, T, AI, CI, NLL, false>(a, p, sc, __builtin_amdgcn_readfirstlane(tk[0]), lds,
+                                             tk, ctr, it);
+}
+
+// Both passes in one persistent launch (schedule: Sched3 mode 2): runs of
+// k3_fwd units and runs of k3_bwd units as the tickets come.
+template <int R, int N, int E, typename T, int AI, int CI, bool NLL>
+__global__ __launch_bounds__(64 * kWV) void k3_fused(SmoothArgs a, Plan3 p, Sched3 sc) {
+  constexpr int LD = fwd_lds_doubles<R>() > bwd_lds_doubles<R, N>() ? fwd_lds_doubles<R>()
+                                                                    : bwd_lds_doubles<R, N>();
+  __shared__ double lds[LD];
+  __shared__ unsigned tk[2];
+  unsigned *ctr = (unsigned *)a.ws;
+  if (threadIdx.x == 0) tk[0] = atomicAdd(ctr, 1u);
+  __syncthreads();
+  unsigned t = __builtin_amdgcn_readfirstlane(tk[0]);
+  int it = 0;
+  while (true) {
+    const Work3 wk = decode3(sc, t);
+    if (wk.phase == 0)
+      t = k3_fwd_run<R, N, E, T, AI, CI, true>(a, p, sc, t, lds, tk, ctr, it);
+    else if (wk.phase == 1)
+      t = k3_bwd_run<R, N, E, T, AI, CI, NLL, true>(a, p, sc, t, lds, tk, ctr, it);
+    else
+      break;
   }
 }
 
@@ -939,6 +1126,18 @@ __global__ __launch_bounds__(64) void k3_nll(SmoothArgs a, Plan3 p) {
 #pragma unroll
   for (int k = 32; k >= 1; k >>= 1) s += __shfl_xor(s, k, 64);
   if (l == 0) a.nll[b] = s;
+}
+
+// One launch for both passes or two (eks_debug_set(EKS_DBG_A3_MODE): 1 = two
+// launches, 2 = one launch, all forward units first, v >= 3 = one launch in
+// batches of v - 2 groups; 0 = the default).  Returns the batch size in
+// groups of the one-launch schedule, 0 for two launches.
+inline long long a3_fused_groups(const Plan3 &p) {
+  const long long m = g_a3_mode;
+  if (m == 1) return 0;
+  if (m == 2) return p.ng;
+  if (m >= 3) return std::min(m - 2, p.ng);
+  return 0;  // default: two launches
 }
 
 // host: the launches of one algo-3 call
@@ -959,21 +1158,38 @@ int launch_algo3_one(const SmoothArgs &a) {
     hipLaunchKernelGGL((k_model_planes<R, N, AI, CI>), dim3(grid_for(a.B, 256)), dim3(256), 0, a.stream,
                        a.params, a.B, (double *)(a.ws + p.prm_off), a.status);
     if ((rc = check_launch("k_model_planes"))) return rc;
-    prof_mark(a.stream, "k3_fwd");
-    hipLaunchKernelGGL((k3_fwd<R, N, EE, Tp, AI, CI>),
-                       dim3(persistent_grid<k3_fwd<R, N, EE, Tp, AI, CI>>(p.units_f)), dim3(64 * kWV), 0,
-                       a.stream, a, p);
-    if ((rc = check_launch("k3_fwd"))) return rc;
-    prof_mark(a.stream, "k3_bwd");
-    if (a.nll)
-      hipLaunchKernelGGL((k3_bwd<R, N, EE, Tp, AI, CI, true>),
-                         dim3(persistent_grid<k3_bwd<R, N, EE, Tp, AI, CI, true>>(p.units)),
-                         dim3(64 * kWV), 0, a.stream, a, p);
-    else
-      hipLaunchKernelGGL((k3_bwd<R, N, EE, Tp, AI, CI, false>),
-                         dim3(persistent_grid<k3_bwd<R, N, EE, Tp, AI, CI, false>>(p.units)),
-                         dim3(64 * kWV), 0, a.stream, a, p);
-    if ((rc = check_launch("k3_bwd"))) return rc;
+    const long long gb = a3_fused_groups(p);
+    if (gb > 0) {  // both passes in one launch
+      prof_mark(a.stream, "k3_fused");
+      const Sched3 sc = make_sched3(p, 2, gb);
+      const long long units = p.units_f + p.units;
+      if (a.nll)
+        hipLaunchKernelGGL((k3_fused<R, N, EE, Tp, AI, CI, true>),
+                           dim3(persistent_grid<k3_fused<R, N, EE, Tp, AI, CI, true>>(units)),
+                           dim3(64 * kWV), 0, a.stream, a, p, sc);
+      else
+        hipLaunchKernelGGL((k3_fused<R, N, EE, Tp, AI, CI, false>),
+                           dim3(persistent_grid<k3_fused<R, N, EE, Tp, AI, CI, false>>(units)),
+                           dim3(64 * kWV), 0, a.stream, a, p, sc);
+      if ((rc = check_launch("k3_fused"))) return rc;
+    } else {
+      prof_mark(a.stream, "k3_fwd");
+      hipLaunchKernelGGL((k3_fwd<R, N, EE, Tp, AI, CI>),
+                         dim3(persistent_grid<k3_fwd<R, N, EE, Tp, AI, CI>>(p.units_f)),
+                         dim3(64 * kWV), 0, a.stream, a, p, make_sched3(p, 0, 0));
+      if ((rc = check_launch("k3_fwd"))) return rc;
+      prof_mark(a.stream, "k3_bwd");
+      const Sched3 sb = make_sched3(p, 1, 0);
+      if (a.nll)
+        hipLaunchKernelGGL((k3_bwd<R, N, EE, Tp, AI, CI, true>),
+                           dim3(persistent_grid<k3_bwd<R, N, EE, Tp, AI, CI, true>>(p.units)),
+                           dim3(64 * kWV), 0, a.stream, a, p, sb);
+      else
+        hipLaunchKernelGGL((k3_bwd<R, N, EE, Tp, AI, CI, false>),
+                           dim3(persistent_grid<k3_bwd<R, N, EE, Tp, AI, CI, false>>(p.units)),
+                           dim3(64 * kWV), 0, a.stream, a, p, sb);
+      if ((rc = check_launch("k3_bwd"))) return rc;
+    }
     if (a.nll) {
       prof_mark(a.stream, "k3_nll");
       hipLaunchKernelGGL((k3_nll<R>), dim3((unsigned)a.B), dim3(64), 0, a.stream, a, p);

@@ -139,3 +139,33 @@ def test_algo3_shard_size_lookback_bit_identical(torch):
     ref = batch.smooth(d[lo:lo + 256], params[lo:lo + 256].contiguous(), n=2, r=2, algo=1,
                        flags=flags)
     assert float((shard[0]["out"][:256] - ref["out"]).abs().max()) < 1e-8
+
+
+@pytest.mark.parametrize("B,T", [(700, 3000), (64, 1000), (2176, 2000)])
+def test_algo3_launch_forms_bit_identical(torch, B, T):
+    """algo 3 as two launches, as one persistent launch with all forward
+    units first, and as one launch whose backward units follow their batch's
+    forward units (batches of 1 and 3 groups): the same operations in the
+    same association order, so the same bits (outputs, smoothed means, NLL);
+    and the forced time-out flags every trajectory in the one-launch form."""
+    from eks_amd import _lib, batch
+    d, params, flags = _singleview(torch, B, T, 900 + B)
+    runs = {}
+    prev = _lib.debug_set(_lib.EKS_DBG_A3_MODE, 1)
+    try:
+        for mode in (1, 2, 3, 5):
+            _lib.debug_set(_lib.EKS_DBG_A3_MODE, mode)
+            runs[mode] = batch.smooth(d, params, n=2, r=2, algo=3, flags=flags, want_ms=True,
+                                      want_nll=True)
+            assert (runs[mode]["status"] == 0).all(), mode
+        _lib.debug_set(_lib.EKS_DBG_A3_MODE, 3)
+        with _Forced():
+            bad = batch.smooth(d, params, n=2, r=2, algo=3, flags=flags)
+            torch.cuda.synchronize()
+            if T > 256:  # (more than one unit per trajectory: every unit but the first waits)
+                assert (bad["status"].cpu().numpy() & _lib.EKS_STATUS_SCAN).all()
+    finally:
+        _lib.debug_set(_lib.EKS_DBG_A3_MODE, prev)
+    for mode in (2, 3, 5):
+        for k in ("out", "ms", "nll"):
+            assert torch.equal(runs[mode][k], runs[1][k]), (mode, k)

@@ -18,13 +18,25 @@ if [ -n "$FULL" ]; then
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || exit $?
   tail -2 $OUT/smoke.log
 fi
+for mode in ${MODES-0}; do
 for nv in ${VIDEOS-1024 128}; do
-  timeout -k 10 300 python bench.py --steps 10 --warmup 2 --no-cpu-baseline --videos $nv > $OUT/bench_v$nv.log 2>&1 || exit $?
-  python - $OUT/bench_v$nv.log $nv <<'PY'
+  timeout -k 10 300 python bench.py --steps 10 --warmup 2 --no-cpu-baseline --videos $nv --a3-mode $mode > $OUT/bench_v${nv}_m$mode.log 2>&1 || exit $?
+  python - $OUT/bench_v${nv}_m$mode.log $nv $mode <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
 k = d["roofline"]["kernels_ms"]
-print(f"v{sys.argv[2]:5s} ms={d['ms_per_step']:.3f} frac={d['roofline']['frac']:.3f} " + " ".join(f"{n}={v:.3f}" for n, v in k.items())
+print(f"v{sys.argv[2]:5s} m{sys.argv[3]} ms={d['ms_per_step']:.3f} frac={d['roofline']['frac']:.3f} " + " ".join(f"{n}={v:.3f}" for n, v in k.items())
       + f" e2e={d['end_to_end']['ms_per_step']:.3f}")
+PY
+done
+done
+for c in ${CONFIGS-}; do
+  timeout -k 10 300 python bench.py --config $c --steps 5 --warmup 1 --no-cpu-baseline > $OUT/bench_c$c.log 2>&1 || exit $?
+  python - $OUT/bench_c$c.log $c <<'PY'
+import json, sys
+d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+e = d.get("end_to_end") or {}
+print(f"c{sys.argv[2]} ms={d['ms_per_step']:.4f} " + " ".join(f"{n}={v:.4f}" for n, v in d["roofline"]["kernels_ms"].items()))
+if e: print(f"   e2e={e['ms_per_step']:.4f} " + " ".join(f"{n}={v:.4f}" for n, v in e["kernels_ms"].items()))
 PY
 done
