@@ -20,8 +20,8 @@
 //   eks::newton_filter(y, ev, mu0, S0, A, Bm, E, max_iter)  eks/newton_eks.py:115-148
 //   eks::interp1d(x, y, xq)                        eks/multiview_pca_smoother.py:86-96
 #include <ATen/ATen.h>
-#include <c10/hip/HIPGuard.h>
-#include <c10/hip/HIPStream.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include <c10/core/DeviceGuard.h>
 #include <torch/library.h>
 
 #include <string>
@@ -33,8 +33,10 @@ namespace {
 
 using at::Tensor;
 
+// (ROCm PyTorch: the HIP device is the "cuda" device type; its streams and
+// guard are the masquerading ones)
 void* cur_stream(const Tensor& t) {
-  return (void*)c10::hip::getCurrentHIPStream(t.device().index()).stream();
+  return (void*)at::hip::getCurrentHIPStreamMasqueradingAsCUDA(t.device().index()).stream();
 }
 
 void check(int rc, const char* what) {
@@ -66,7 +68,7 @@ Tensor contiguous_f64(const Tensor& t) { return t.to(at::kDouble).contiguous(); 
 std::tuple<Tensor, Tensor> ensemble_gpu(const Tensor& obs, const std::string& mode) {
   need_gpu(obs, "obs");
   TORCH_CHECK(obs.dim() == 4, "obs must be viewed as (B, T, E, n)");
-  const c10::hip::HIPGuard g(obs.device());
+  const c10::DeviceGuard g(obs.device());
   const int64_t B = obs.size(0), T = obs.size(1), E = obs.size(2), n = obs.size(3);
   Tensor preds = at::empty({B, T, n}, f64(obs));
   Tensor vars = at::empty({B, T, n}, f64(obs));
@@ -94,7 +96,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> forward_gpu(const Tensor& y, 
                                                                const Tensor& C) {
   need_gpu(y, "y");
   TORCH_CHECK(y.dim() == 3 && ev.sizes() == y.sizes(), "y and ev must both be (B, T, n)");
-  const c10::hip::HIPGuard g(y.device());
+  const c10::DeviceGuard g(y.device());
   const int64_t B = y.size(0), T = y.size(1), n = y.size(2), r = m0.size(-1);
   const int shared = m0.dim() == 1 ? 1 : 0;
   Tensor y_ = contiguous_f64(y), ev_ = contiguous_f64(ev);
@@ -128,7 +130,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> backward_gpu(const Tensor& mf, const 
                                                         const Tensor& S, const Tensor& A) {
   need_gpu(mf, "mf");
   TORCH_CHECK(mf.dim() == 3, "mf must be (B, T, r)");
-  const c10::hip::HIPGuard g(mf.device());
+  const c10::DeviceGuard g(mf.device());
   const int64_t B = mf.size(0), T = mf.size(1), r = mf.size(2);
   const int shared = A.dim() == 2 ? 1 : 0;
   Tensor mf_ = contiguous_f64(mf), Vf_ = contiguous_f64(Vf), S_ = contiguous_f64(S);
@@ -161,7 +163,7 @@ std::tuple<Tensor, Tensor, Tensor> smooth_impl(const Tensor& obs, const Tensor& 
   need_gpu(obs, "obs");
   need_gpu(params, "params");
   TORCH_CHECK(obs.dim() == 4 && obs.size(3) == n, "obs must be viewed as (B, T, E, n) with n=", n);
-  const c10::hip::HIPGuard g(obs.device());
+  const c10::DeviceGuard g(obs.device());
   const int64_t B = obs.size(0), T = obs.size(1), E = obs.size(2);
   Tensor prm = params.contiguous();
   TORCH_CHECK(prm.scalar_type() == at::kDouble && prm.dim() == 2 && prm.size(0) == B &&
@@ -223,7 +225,7 @@ std::tuple<Tensor, Tensor> fit_gpu(const Tensor& obs, const std::string& kind, i
   need_gpu(obs, "obs");
   TORCH_CHECK(obs.dim() == 4 && obs.size(3) == n, "obs must be viewed as (B, T, E, n) with n=", n);
   TORCH_CHECK(kind == "singleview" || kind == "multicam", "kind must be singleview or multicam");
-  const c10::hip::HIPGuard g(obs.device());
+  const c10::DeviceGuard g(obs.device());
   const int64_t B = obs.size(0), T = obs.size(1), E = obs.size(2);
   Tensor params = at::empty({B, eks_param_len((int)n, (int)r)}, f64(obs));
   Tensor status = at::empty({B}, i32(obs));
@@ -249,7 +251,7 @@ std::tuple<Tensor, Tensor> newton_gpu(const Tensor& y, const Tensor& ev, const T
                                       const Tensor& E, int64_t max_iter) {
   need_gpu(y, "y");
   TORCH_CHECK(y.dim() == 3 && ev.sizes() == y.sizes(), "y and ev must both be (B, T, n)");
-  const c10::hip::HIPGuard g(y.device());
+  const c10::DeviceGuard g(y.device());
   const int64_t B = y.size(0), T = y.size(1), n = y.size(2), r = mu0.size(-1);
   const int shared = mu0.dim() == 1 ? 1 : 0;
   Tensor y_ = contiguous_f64(y), ev_ = contiguous_f64(ev), mu0_ = contiguous_f64(mu0);
@@ -276,7 +278,7 @@ Tensor interp_gpu(const Tensor& x, const Tensor& y, const Tensor& xq) {
   need_gpu(x, "x");
   TORCH_CHECK(y.dim() == 2 && x.dim() == 1 && xq.dim() == 1 && y.size(0) == x.size(0),
               "x (n,), y (n, C), xq (q,)");
-  const c10::hip::HIPGuard g(x.device());
+  const c10::DeviceGuard g(x.device());
   Tensor x_ = contiguous_f64(x), y_ = y.to(at::kDouble), xq_ = contiguous_f64(xq);
   const int64_t n = x_.size(0), C = y_.size(1), q = xq_.size(0);
   Tensor out = at::empty({q, C}, f64(x));

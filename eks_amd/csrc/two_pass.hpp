@@ -1158,8 +1158,11 @@ int launch_algo3_one(const SmoothArgs &a) {
     hipLaunchKernelGGL((k_model_planes<R, N, AI, CI>), dim3(grid_for(a.B, 256)), dim3(256), 0, a.stream,
                        a.params, a.B, (double *)(a.ws + p.prm_off), a.status);
     if ((rc = check_launch("k_model_planes"))) return rc;
-    const long long gb = a3_fused_groups(p);
-    if (gb > 0) {  // both passes in one launch
+    // (the one-launch form is compiled for the single-view model only: the
+    // throughput shape; others keep two launches)
+    constexpr bool kCanFuse = R == 2 && N == 2 && AI == kAId && CI == kCId;
+    const long long gb = kCanFuse ? a3_fused_groups(p) : 0;
+    if constexpr (kCanFuse) if (gb > 0) {  // both passes in one launch
       prof_mark(a.stream, "k3_fused");
       const Sched3 sc = make_sched3(p, 2, gb);
       const long long units = p.units_f + p.units;
@@ -1172,7 +1175,8 @@ int launch_algo3_one(const SmoothArgs &a) {
                            dim3(persistent_grid<k3_fused<R, N, EE, Tp, AI, CI, false>>(units)),
                            dim3(64 * kWV), 0, a.stream, a, p, sc);
       if ((rc = check_launch("k3_fused"))) return rc;
-    } else {
+    }
+    if (!kCanFuse || gb <= 0) {
       prof_mark(a.stream, "k3_fwd");
       hipLaunchKernelGGL((k3_fwd<R, N, EE, Tp, AI, CI>),
                          dim3(persistent_grid<k3_fwd<R, N, EE, Tp, AI, CI>>(p.units_f)),
