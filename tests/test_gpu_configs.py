@@ -124,6 +124,15 @@ def test_config5_pupil_1M_sweep_and_smooth(torch):
     assert bool(torch.isfinite(s_auto).all())
     best = int(torch.argmin(s_auto))
     assert best == int(torch.argmin(s_seq))
+    # the kernels the bench times: EKS_MODEL_PUPIL (sparse pupil rows, folded
+    # equal rows, diagonal A / Q)
+    from eks_amd import _lib
+    flags = batch.model_flags(stk("A"), stk("C"), stk("Q"))
+    assert flags & _lib.EKS_MODEL_PUPIL
+    s_pup = batch.nll(cobs, params, n=8, r=3, flags=flags)
+    rel = float(((s_pup - s_seq) / s_seq.abs()).abs().max())
+    assert rel < NLL_RTOL, rel
+    assert int(torch.argmin(s_pup)) == best
     p_best = params[best:best + 1].contiguous()
     ref = _algos_agree(torch, obs, p_best, 8, 3, 0, [2])
     # oracle: the chosen model refitted on a 200k-frame prefix, smoothed on both sides
@@ -135,6 +144,11 @@ def test_config5_pupil_1M_sweep_and_smooth(torch):
     g = batch.smooth(obs[:, :Tc], pb, n=8, r=3, check=True)["out"][0].cpu().numpy()
     d = float(np.abs(g - markers).max())
     assert d < PX_CPU, d
+    fb = batch.model_flags(pm["A"][None], pm["C"][None], pm["Q"][None])
+    assert fb & _lib.EKS_MODEL_PUPIL
+    gp = batch.smooth(obs[:, :Tc], pb, n=8, r=3, flags=fb, check=True)["out"][0].cpu().numpy()
+    d = float(np.abs(gp - markers).max())
+    assert d < PX_CPU, d
     # the sweep's NLL against the oracle's definition on a 20k-frame prefix
     Tn = 20000
     pre = st[:, :Tn].astype(np.float64)
@@ -143,5 +157,8 @@ def test_config5_pupil_1M_sweep_and_smooth(torch):
         c = cands[i]
         want = O.compute_nll(pp - c["offset"], c["m0"], c["S0"], c["C"], c["A"], c["Q"], ev)
         got = float(batch.nll(obs[:, :Tn], params[i:i + 1].contiguous(), n=8, r=3)[0])
+        assert math.isclose(got, want, rel_tol=1e-9), (i, got, want)
+        got = float(batch.nll(obs[:, :Tn], params[i:i + 1].contiguous(), n=8, r=3,
+                              flags=flags)[0])
         assert math.isclose(got, want, rel_tol=1e-9), (i, got, want)
     del ref
