@@ -447,15 +447,16 @@ template <int R>
 constexpr int fwd_lds_doubles() {
   return ((fwd_fpw<R>() > 1 ? kWV : 1) + kWV) * Elem<R>::len * 64 + (R + Sym<R>::len) * 64;
 }
-// k3_fused's forward member loads: default cache policy, so that the
-// backward units of the same batch find the members in the Infinity Cache
-constexpr bool kFusedFwdNt = false;
 
 // The k3_fwd units of consecutive tickets from t on (a run ends at the
 // first ticket that is not a k3_fwd unit, which is returned).  FUSED: the
 // fine start states are stored write-through and each unit sets its
 // flag3 word once they are (k3_fused's backward units wait for it).
-template <int R, int N, int E, typename T, int AI, int CI, bool FUSED>
+// FWD_NT: non-temporal member loads (the two-launch form and the one-launch
+// form with all forward units first: nothing re-reads them soon); the batched
+// one-launch form loads them with the default policy, so that the backward
+// units one batch later find them in the Infinity Cache.
+template <int R, int N, int E, typename T, int AI, int CI, bool FUSED, bool FWD_NT = kNtLoad>
 EKS_DEV unsigned k3_fwd_run(const SmoothArgs &a, const Plan3 &p, const Sched3 &sc, unsigned t,
                             double *lds, unsigned *tk, unsigned *ctr, int &it) {
   constexpr int EL = Elem<R>::len, KS = R + Sym<R>::len;
@@ -474,7 +475,7 @@ EKS_DEV unsigned k3_fwd_run(const SmoothArgs &a, const Plan3 &p, const Sched3 &s
   double *agg1 = (double *)(a.ws + p.agg1_off);
   const double *prm = (const double *)(a.ws + p.prm_off);
   // member ring, persists across the units of the run
-  typename SrcOf<E, N, T, D, FUSED ? kFusedFwdNt : kNtLoad>::type src;
+  typename SrcOf<E, N, T, D, FWD_NT>::type src;
   src.init(a);
   Model<R, N> md;
   // model + the first member steps of unit wk (structure checked by
@@ -1092,7 +1093,7 @@ __global__ __launch_bounds__(64 * kWV) void k3_bwd(SmoothArgs a, Plan3 p, Sched3
 
 // Both passes in one persistent launch (schedule: Sched3 mode 2): runs of
 // k3_fwd units and runs of k3_bwd units as the tickets come.
-template <int R, int N, int E, typename T, int AI, int CI, bool NLL>
+template <int R, int N, int E, typename T, int AI, int CI, bool NLL, bool FWD_NT>
 __global__ __launch_bounds__(64 * kWV) void k3_fused(SmoothArgs a, Plan3 p, Sched3 sc) {
   constexpr int LD = fwd_lds_doubles<R>() > bwd_lds_doubles<R, N>() ? fwd_lds_doubles<R>()
                                                                     : bwd_lds_doubles<R, N>();
@@ -1106,7 +1107,7 @@ __global__ __launch_bounds__(64 * kWV) void k3_fused(SmoothArgs a, Plan3 p, Sche
   while (true) {
     const Work3 wk = decode3(sc, t);
     if (wk.phase == 0)
-      t = k3_fwd_run<R, N, E, T, AI, CI, true>(a, p, sc, t, lds, tk, ctr, it);
+      t = k3_fwd_run<R, N, E, T, AI, CI, true, FWD_NT>(a, p, sc, t, lds, tk, ctr, it);
     else if (wk.phase == 1)
       t = k3_bwd_run<R, N, E, T, AI, CI, NLL, true>(a, p, sc, t, lds, tk, ctr, it);
     else
@@ -1166,14 +1167,26 @@ int launch_algo3_one(const SmoothArgs &a) {
       prof_mark(a.stream, "k3_fused");
       const Sched3 sc = make_sched3(p, 2, gb);
       const long long units = p.units_f + p.units;
-      if (a.nll)
-        hipLaunchKernelGGL((k3_fused<R, N, EE, Tp, AI, CI, true>),
-                           dim3(persistent_grid<k3_fused<R, N, EE, Tp, AI, CI, true>>(units)),
-                           dim3(64 * kWV), 0, a.stream, a, p, sc);
-      else
-        hipLaunchKernelGGL((k3_fused<R, N, EE, Tp, AI, CI, false>),
-                           dim3(persistent_grid<k3_fused<R, N, EE, Tp, AI, CI, false>>(units)),
-                           dim3(64 * kWV), 0, a.stream, a, p, sc);
+      const bool batched = sc.NB > 1;  // default-policy forward loads (MALL re-read)
+      if (a.nll) {
+        if (batched)
+          hipLaunchKernelGGL((k3_fused<R, N, EE, Tp, AI, CI, true, false>),
+                             dim3(persistent_grid<k3_fused<R, N, EE, Tp, AI, CI, true, false>>(units)),
+                             dim3(64 * kWV), 0, a.stream, a, p, sc);
+        else
+          hipLaunchKernelGGL((k3_fused<R, N, EE, Tp, AI, CI, true, true>),
+                             dim3(persistent_grid<k3_fused<R, N, EE, Tp, AI, CI, true, true>>(units)),
+                             dim3(64 * kWV), 0, a.stream, a, p, sc);
+      } else {
+        if (batched)
+          hipLaunchKernelGGL((k3_fused<R, N, EE, Tp, AI, CI, false, false>),
+                             dim3(persistent_grid<k3_fused<R, N, EE, Tp, AI, CI, false, false>>(units)),
+                             dim3(64 * kWV), 0, a.stream, a, p, sc);
+        else
+          hipLaunchKernelGGL((k3_fused<R, N, EE, Tp, AI, CI, false, true>),
+                             dim3(persistent_grid<k3_fused<R, N, EE, Tp, AI, CI, false, true>>(units)),
+                             dim3(64 * kWV), 0, a.stream, a, p, sc);
+      }
       if ((rc = check_launch("k3_fused"))) return rc;
     }
     if (!kCanFuse || gb <= 0) {
