@@ -164,10 +164,23 @@ struct MemberRing {
   }
   EKS_DEV void fetch(int slot, long long t) {
     const __amdgpu_buffer_rsrc_t rs = member_rsrc(base + t * stb);
+    // the E x N member offsets are rebuilt from the two strides at every
+    // fetch (one scalar add each) instead of being hoisted out of the step
+    // loop: ten loop-invariant offsets overflowed the SGPR file, and each
+    // load then paid a v_readlane + 4 wait states to get its offset back
+    int seb_ = seb, sjb_ = sjb;
+    asm volatile("" : "+s"(seb_), "+s"(sjb_));
+    int off_e = 0;
 #pragma unroll
-    for (int e = 0; e < E; ++e)
+    for (int e = 0; e < E; ++e) {
+      int off = off_e;
 #pragma unroll
-      for (int j = 0; j < N; ++j) v[slot][e][j] = member_load<T, NT>(rs, loff, e * seb + j * sjb);
+      for (int j = 0; j < N; ++j) {
+        v[slot][e][j] = member_load<T, NT>(rs, loff, off);
+        off += sjb_;
+      }
+      off_e += seb_;
+    }
   }
   EKS_DEV void get(int slot, double (&avg)[N], double (&rv)[N]) const {
 #pragma unroll
