@@ -205,7 +205,7 @@ def test_quantised_members_keep_reference_frames(torch, name):
     """Members on a 0.25 px grid (E = 3 and 5): the worst variances tie in
     large groups, so the percentile threshold equals many frames' values.
     The device ensemble (mean and variance scaled by 1/E and 1/E^2, within
-    1-2 ulp of numpy's / E: ensemble.hpp) and the device fit (eks_fit, both
+    4 ulp of numpy's / E: ensemble.hpp) and the device fit (eks_fit, both
     selection paths) must keep exactly the frames the reference keeps
     (``good`` in the fixture, eks/multiview_pca_smoother.py:685-688's rule
     applied by tools/gen_golden.py with the reference's ensemble): the
@@ -216,9 +216,10 @@ def test_quantised_members_keep_reference_frames(torch, name):
     obs = g["obs"]  # (E, T, 2), float32-exact
     d = batch.make_time_major(obs[None], dtype=np.float32)
     import eks_amd.ops  # noqa: F401
-    # the ensemble variances: equal to the reference's to 2 ulp
+    # the ensemble variances: within 4 ulp of the reference's (mean and
+    # variance scaled by the rounded 1/E, 1/E^2 instead of numpy's divisions)
     _, ev = torch.ops.eks.ensemble(d, "median")
-    np.testing.assert_allclose(ev[0].cpu().numpy(), g["ev"], rtol=4.5e-16, atol=0)
+    np.testing.assert_allclose(ev[0].cpu().numpy(), g["ev"], rtol=9e-16, atol=0)
     for sel in (1, 2):
         prev = _lib.debug_set(_lib.EKS_DBG_FIT_SELECT, sel)
         try:
