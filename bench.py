@@ -81,8 +81,7 @@ def parse():
                     help="launch every step eagerly instead of replaying a captured HIP graph")
     ap.add_argument("--a3-mode", type=int, default=0,
                     help="tuning: algo 3's launch form (eks_debug_set EKS_DBG_A3_MODE: 0 default, "
-                         "1 two launches, 2 one launch, v >= 3 one launch in batches of v - 2 "
-                         "groups)")
+                         "1 two launches, 2 one launch)")
     ap.add_argument("--scaling", choices=["strong", "weak"], default="strong",
                     help="config 4: strong = the video batch is split over ranks; weak = "
                          "every rank smooths --videos videos")

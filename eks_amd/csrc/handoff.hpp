@@ -92,12 +92,14 @@ EKS_DEV bool wait_flag_lanes(const unsigned *flag, bool need, long long wait_tic
 // kAggReady = the unit's own aggregate published, kIncReady = its inclusive
 // value published).  Starting at unit `j` and stepping by `step` (-1: towards
 // earlier units), returns the first unit whose inclusive value is published;
-// every unit passed on the way has its aggregate published.  Units that have
-// published nothing are waited for (each wait bounded as wait_flag); on
-// timeout `ok` is cleared and the search stops at the unit it waited for
-// (whose payload is then stale: the caller's result is flagged, not used).
-// Units published by smaller tickets always publish their aggregate before
-// they wait for anything, so the search ends.
+// every unit passed on the way has its aggregate published.  The 64 lanes of
+// the wave read 64 consecutive flags of the walk at once (one load round
+// trip per window instead of one per unit: a poll waits behind the CU's
+// streaming loads); units that have published nothing yet are polled again.
+// On timeout `ok` is cleared and the search stops (the caller's value is
+// then stale and flagged, not used).  Units with smaller tickets publish
+// their aggregate before they wait for anything, and the first unit of the
+// chain publishes its inclusive value directly, so the search ends.
 constexpr unsigned kAggReady = 1u, kIncReady = 2u;
 // the fast path: is unit j's inclusive value already published?
 EKS_DEV bool inc_ready(const unsigned *flag, long long wait_ticks) {
@@ -107,26 +109,38 @@ EKS_DEV bool inc_ready(const unsigned *flag, long long wait_ticks) {
   return true;
 }
 EKS_DEV long long look_back(const unsigned *flags, long long j, long long stride, int step,
-                            long long wait_ticks, bool &ok) {
+                            long long nunits, long long wait_ticks, bool &ok) {
   if (wait_ticks < 0) {  // fault injection (tests): give up at once
     ok = false;
     return j;
   }
+  const int l = threadIdx.x & 63;
+  Deadline dl(wait_ticks);
+  long long base = j;
   while (true) {
-    Deadline dl(wait_ticks);
-    unsigned f;
-    while ((f = (unsigned)__builtin_amdgcn_readfirstlane(ld_flag(flags + j * stride))) == 0u) {
-      if (dl.expired()) {
-        ok = false;
-        return j;
+    const long long u = base + (long long)step * l;
+    const bool valid = u >= 0 && u < nunits;
+    const unsigned f = valid ? ld_flag(flags + u * stride) : 0u;
+    const unsigned long long inc = __ballot(valid && f >= kIncReady);
+    const unsigned long long none = __ballot(valid && f == 0u);
+    const unsigned long long all = __ballot(valid);
+    if (inc) {
+      const int k0 = __ffsll((long long)inc) - 1;  // the nearest inclusive value
+      const unsigned long long before = k0 == 0 ? 0ull : ((1ull << k0) - 1ull);
+      if ((none & before) == 0ull) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        return base + (long long)step * k0;
       }
-      __builtin_amdgcn_s_sleep(1);
+    } else if (none == 0ull && all == ~0ull) {
+      base += (long long)step * 64;  // 64 aggregates: look further
+      continue;
     }
-    if (f >= kIncReady) break;
-    j += step;
+    if (dl.expired()) {
+      ok = false;
+      return base;
+    }
+    __builtin_amdgcn_s_sleep(1);
   }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  return j;
 }
 
 }  // namespace eks

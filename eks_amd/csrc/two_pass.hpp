@@ -657,7 +657,7 @@ EKS_DEV unsigned k3_fwd_run(const SmoothArgs &a, const Plan3 &p, const Sched3 &s
             if (lane_ok) elem_store_pl_wt<R>(Ec, agg1, cu * EL, B, b);
             publish_flag(flags + cu * p.ng + grp, l, kAggReady);
           }
-          j = look_back(fl, j, p.ng, -1, a.wait_ticks, ok);
+          j = look_back(fl, j, p.ng, -1, p.NCu, a.wait_ticks, ok);
         }
         if (lane_ok) {
           state_load_pl_wt<R>(fst, ((j + 1) * KPU) * KS, B, b, m, P);
@@ -941,7 +941,7 @@ EKS_DEV unsigned k3_bwd_run(const SmoothArgs &a, const Plan3 &p, const Sched3 &s
             }
             publish_flag(flags + cc * p.ng + grp, l, kAggReady);
           }
-          j = look_back(fl, j, p.ng, +1, a.wait_ticks, okc);
+          j = look_back(fl, j, p.ng, +1, p.NCc, a.wait_ticks, okc);
         }
         if (lane_ok) {
 #pragma unroll
@@ -1143,15 +1143,14 @@ __global__ __launch_bounds__(64) void k3_nll(SmoothArgs a, Plan3 p) {
 }
 
 // One launch for both passes or two (eks_debug_set(EKS_DBG_A3_MODE): 1 = two
-// launches, 2 = one launch, all forward units first, v >= 3 = one launch in
-// batches of v - 2 groups; 0 = the default).  Returns the batch size in
-// groups of the one-launch schedule, 0 for two launches.
+// launches, 2 = one launch, all forward units first; 0 = the default, two
+// launches: measured equal at config 4 and its 8-GPU shard).
+// Returns the batch size in groups of the one-launch schedule, 0 for two
+// launches.  (The batched schedule, small GB, was measured 5-15x slower: with
+// one or a few groups per batch the chains of a batch run nearly alone on
+// the chip; it is kept in decode3 but not launched.)
 inline long long a3_fused_groups(const Plan3 &p) {
-  const long long m = g_a3_mode;
-  if (m == 1) return 0;
-  if (m == 2) return p.ng;
-  if (m >= 3) return std::min(m - 2, p.ng);
-  return 0;  // default: two launches
+  return g_a3_mode >= 2 ? p.ng : 0;
 }
 
 // host: the launches of one algo-3 call
@@ -1180,26 +1179,14 @@ int launch_algo3_one(const SmoothArgs &a) {
       prof_mark(a.stream, "k3_fused");
       const Sched3 sc = make_sched3(p, 2, gb);
       const long long units = p.units_f + p.units;
-      const bool batched = sc.NB > 1;  // default-policy forward loads (MALL re-read)
-      if (a.nll) {
-        if (batched)
-          hipLaunchKernelGGL((k3_fused<R, N, EE, Tp, AI, CI, true, false>),
-                             dim3(persistent_grid<k3_fused<R, N, EE, Tp, AI, CI, true, false>>(units)),
-                             dim3(64 * kWV), 0, a.stream, a, p, sc);
-        else
-          hipLaunchKernelGGL((k3_fused<R, N, EE, Tp, AI, CI, true, true>),
-                             dim3(persistent_grid<k3_fused<R, N, EE, Tp, AI, CI, true, true>>(units)),
-                             dim3(64 * kWV), 0, a.stream, a, p, sc);
-      } else {
-        if (batched)
-          hipLaunchKernelGGL((k3_fused<R, N, EE, Tp, AI, CI, false, false>),
-                             dim3(persistent_grid<k3_fused<R, N, EE, Tp, AI, CI, false, false>>(units)),
-                             dim3(64 * kWV), 0, a.stream, a, p, sc);
-        else
-          hipLaunchKernelGGL((k3_fused<R, N, EE, Tp, AI, CI, false, true>),
-                             dim3(persistent_grid<k3_fused<R, N, EE, Tp, AI, CI, false, true>>(units)),
-                             dim3(64 * kWV), 0, a.stream, a, p, sc);
-      }
+      if (a.nll)
+        hipLaunchKernelGGL((k3_fused<R, N, EE, Tp, AI, CI, true, true>),
+                           dim3(persistent_grid<k3_fused<R, N, EE, Tp, AI, CI, true, true>>(units)),
+                           dim3(64 * kWV), 0, a.stream, a, p, sc);
+      else
+        hipLaunchKernelGGL((k3_fused<R, N, EE, Tp, AI, CI, false, true>),
+                           dim3(persistent_grid<k3_fused<R, N, EE, Tp, AI, CI, false, true>>(units)),
+                           dim3(64 * kWV), 0, a.stream, a, p, sc);
       if ((rc = check_launch("k3_fused"))) return rc;
     }
     if (!kCanFuse || gb <= 0) {

@@ -326,12 +326,10 @@ int eks_interp1d(const double *x, int64_t nx, const double *y, int64_t ncol, int
  *                          one block per row, 2 = split (both must give the
  *                          same threshold and kept-frame mask).  The
  *                          workspace size follows the setting.
- *   EKS_DBG_A3_MODE        algo 3's launch form: 0 = the default, 1 = two
- *                          launches (forward pass, backward pass), 2 = one
- *                          persistent launch, all forward units first, v >= 3
- *                          = one launch with the backward units of each batch
- *                          of v - 2 64-trajectory groups one batch behind its
- *                          forward units.  Results are bit-identical in all.
+ *   EKS_DBG_A3_MODE        algo 3's launch form: 0 = the default (two
+ *                          launches), 1 = two launches (forward pass,
+ *                          backward pass), 2 = one persistent launch, all
+ *                          forward units first.  Results are bit-identical.
  */
 enum { EKS_DBG_WAIT_US = 1, EKS_DBG_A3_SLICE_BYTES = 2, EKS_DBG_FIT_SELECT = 3,
        EKS_DBG_A3_MODE = 4 };
