@@ -600,6 +600,10 @@ __global__ __launch_bounds__(256) void k_sel_cand(const double *__restrict__ wor
   if (!nan && above != ~0ull) atomicMin(&row.above, above);
 }
 
+// candidates of the split selection held in LDS (128 KB: the kernel runs one
+// 1024-thread block per row, few rows)
+constexpr int kCandBig = 16384;
+
 template <int BLK>
 __global__ __launch_bounds__(BLK) void k_sel_final(const double *__restrict__ worst, long long TT,
                                                    long long hi_minus_lo, double g,
@@ -609,7 +613,7 @@ __global__ __launch_bounds__(BLK) void k_sel_final(const double *__restrict__ wo
                                                    double *__restrict__ thr,
                                                    uint64_t *__restrict__ kept, long long W) {
   __shared__ unsigned hsel[1 << kSelDigit];
-  __shared__ uint64_t cand[kCand];
+  __shared__ uint64_t cand[kCandBig];
   __shared__ uint64_t su[4];
   __shared__ long long si[2 + BLK / 64];
   const long long b = blockIdx.x;
@@ -626,7 +630,7 @@ __global__ __launch_bounds__(BLK) void k_sel_final(const double *__restrict__ wo
   constexpr int lo_bit = 51;
   uint64_t ka;
   const uint64_t *src = ck;
-  if (cnt <= kCand) {
+  if (cnt <= kCandBig) {
     for (long long i = threadIdx.x; i < cnt; i += BLK) cand[i] = ck[i];
     __syncthreads();
     src = cand;
@@ -1272,8 +1276,8 @@ extern "C" int eks_fit(const void *obs, int obs_dtype, int64_t B, int64_t T, int
           hipLaunchKernelGGL(k_sel_bin, dim3((unsigned)B), dim3(256), 0, s, ghist, lo, rows);
           hipLaunchKernelGGL(k_sel_cand, dim3(gs), dim3(256), 0, s, worst, T, G, rows, ckey, cidx,
                              yev ? kept : nullptr, W);
-          hipLaunchKernelGGL(k_sel_final<256>, dim3((unsigned)B), dim3(256), 0, s, worst, T, hi - lo,
-                             g, rows, ckey, cidx, thr, yev ? kept : nullptr, W);
+          hipLaunchKernelGGL(k_sel_final<1024>, dim3((unsigned)B), dim3(1024), 0, s, worst, T,
+                             hi - lo, g, rows, ckey, cidx, thr, yev ? kept : nullptr, W);
         } else if (T >= 65536) {
           hipLaunchKernelGGL(k_fit_select<1024>, dim3((unsigned)B), dim3(1024), 0, s, worst, T,
                              lo, hi, g, thr, yev ? kept : nullptr, W);

@@ -107,19 +107,21 @@ def test_mask_long_rows_whole_row_pass(torch):
     _vs_host(st, p, 25.0)
 
 
-def test_mask_bin_larger_than_lds(torch):
+@pytest.mark.parametrize("T,big", [(40000, 4096), (160000, 16384)])
+def test_mask_bin_larger_than_lds(torch, T, big):
     """No outliers and long rows: the threshold's top-digit bin holds more
-    frames than the LDS candidate buffer (3 072), so the select runs over the
-    global row and the mask comes from the whole-row pass."""
+    frames than the LDS candidate buffer (3 072 for one block per row, 16 384
+    for the split selection's final block), so the select runs over the
+    global row / candidate buffer and the mask comes from the whole-row pass."""
     from eks_amd import synthetic
     from eks_amd.core import ensemble_array
-    rng = np.random.default_rng(20000)
-    T, q = 40000, 40.0
+    rng = np.random.default_rng(20000 + T)
+    q = 40.0
     st = np.stack([synthetic.singleview_obs(rng, 5, T, outlier_frac=0.0)[:, :, 0]
                    for _ in range(3)])
     v = np.sort(ensemble_array(st[0].astype(np.float64))[1].max(axis=1))
     key = v.view(np.uint64) >> 51
-    assert (key == key[int((T - 1) * q / 100)]).sum() > 4096
+    assert (key == key[int((T - 1) * q / 100)]).sum() > big
     p = _fit_both(torch, st, q)
     _vs_host(st, p, q)
 
