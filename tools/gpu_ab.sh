@@ -23,3 +23,14 @@ print(f"{sys.argv[2][-30:]:30s} v{sys.argv[3]:5s} ms={d['ms_per_step']:.3f} frac
 PY
   done
 done
+unset EKS_LIB
+for c in ${CONFIGS-}; do
+  timeout -k 10 300 python bench.py --config $c --steps 5 --warmup 1 --no-cpu-baseline > $OUT/bench_c$c.log 2>&1 || exit $?
+  python - $OUT/bench_c$c.log $c <<'PY'
+import json, sys
+d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+e = d.get("end_to_end") or {}
+print(f"c{sys.argv[2]} ms={d['ms_per_step']:.4f} " + " ".join(f"{n}={v:.4f}" for n, v in d["roofline"]["kernels_ms"].items()))
+if e: print(f"   e2e={e['ms_per_step']:.4f} " + " ".join(f"{n}={v:.4f}" for n, v in e["kernels_ms"].items()))
+PY
+done
