@@ -397,18 +397,22 @@ inline Sched3 make_sched3(const Plan3 &p, int mode, long long gb) {
   s.NCc = p.NCc;
   return s;
 }
-EKS_DEV Work3 decode3(const Sched3 &s, unsigned long long t) {
+// MODE: the kernel's schedule (0 / 1: one pass, 32-bit arithmetic only; 2:
+// the one-launch schedule)
+template <int MODE>
+EKS_DEV Work3 decode3(const Sched3 &s, unsigned t) {
   Work3 w{2, 0, 0};
-  const long long tt = (long long)t;
-  if (s.mode != 2) {
-    const long long nc = s.mode == 0 ? s.NCu : s.NCc;
-    if (tt < nc * s.ng) {
-      w.phase = s.mode;
-      w.c = tt / s.ng;
-      w.grp = tt - w.c * s.ng;
+  if constexpr (MODE != 2) {
+    const unsigned nc = (unsigned)(MODE == 0 ? s.NCu : s.NCc), ng = (unsigned)s.ng;
+    if (t < nc * ng) {
+      const unsigned c = t / ng;
+      w.phase = MODE;
+      w.c = c;
+      w.grp = t - c * ng;
     }
     return w;
   }
+  const long long tt = (long long)t;
   auto seg = [&](int ph, long long batch, long long l) {
     const long long gk = batch == s.NB - 1 ? s.gl : s.GB;
     w.phase = ph;
@@ -515,7 +519,7 @@ EKS_DEV unsigned k3_fwd_run(const SmoothArgs &a, const Plan3 &p, const Sched3 &s
 #pragma unroll
       for (int j = i; j < R; ++j) P[i][j] = P[j][i] = shS[k++][l];
   };
-  Work3 wk = decode3(sc, t);  // uniform: every index below in SGPRs
+  Work3 wk = decode3<FUSED ? 2 : 0>(sc, t);  // uniform: every index below in SGPRs
   head(wk);
   while (wk.phase == 0) {
     unsigned tnext = 0;
@@ -604,7 +608,7 @@ EKS_DEV unsigned k3_fwd_run(const SmoothArgs &a, const Plan3 &p, const Sched3 &s
     if (threadIdx.x == 0) tk[(it + 1) & 1] = tnext;
     __syncthreads();
     const unsigned tn = __builtin_amdgcn_readfirstlane(tk[(it + 1) & 1]);
-    const Work3 wn = decode3(sc, tn);
+    const Work3 wn = decode3<FUSED ? 2 : 0>(sc, tn);
     // the next unit's first member steps in flight during this unit's tail
     // (wave 0 after its chain wait: vmcnt counts in order, so a prefetch
     // issued before the poll would hold the poll back until it lands)
@@ -650,14 +654,14 @@ EKS_DEV unsigned k3_fwd_run(const SmoothArgs &a, const Plan3 &p, const Sched3 &s
         for (int j = 0; j < R; ++j) P[i][j] = 0.0;
       }
       if (cu > 0) {
-        const unsigned *fl = flags + grp;
+        const unsigned *fl = flags + grp * p.NCu;  // group-major: a walk reads consecutive words
         long long j = cu - 1;
-        if (!inc_ready(fl + j * p.ng, a.wait_ticks)) {
+        if (!inc_ready(fl + j, a.wait_ticks)) {
           if (cu + 1 < p.NCu) {
             if (lane_ok) elem_store_pl_wt<R>(Ec, agg1, cu * EL, B, b);
-            publish_flag(flags + cu * p.ng + grp, l, kAggReady);
+            publish_flag(flags + grp * p.NCu + cu, l, kAggReady);
           }
-          j = look_back(fl, j, p.ng, -1, p.NCu, a.wait_ticks, ok);
+          j = look_back(fl, j, 1, -1, p.NCu, a.wait_ticks, ok);
         }
         if (lane_ok) {
           state_load_pl_wt<R>(fst, ((j + 1) * KPU) * KS, B, b, m, P);
@@ -688,7 +692,7 @@ EKS_DEV unsigned k3_fwd_run(const SmoothArgs &a, const Plan3 &p, const Sched3 &s
       ok = compose_state<R>(m, P, Ec) && ok;  // the state leaving unit cu
       if (cu + 1 < p.NCu) {
         if (lane_ok) state_store_pl_wt<R>(fst, ((cu + 1) * KPU) * KS, B, b, m, P);
-        publish_flag(flags + cu * p.ng + grp, l, kIncReady);
+        publish_flag(flags + grp * p.NCu + cu, l, kIncReady);
       }
       head(wn);
     }
@@ -780,7 +784,7 @@ EKS_DEV unsigned k3_bwd_run(const SmoothArgs &a, const Plan3 &p, const Sched3 &s
   const double *prm = (const double *)(a.ws + p.prm_off);
   const bool vec2 = N == 2 && a.oj == 1 && ((a.ob | a.ot) & 1) == 0 &&
                     (((uintptr_t)a.out) & 15) == 0;
-  Work3 wk = decode3(sc, t);  // uniform: every index below in SGPRs
+  Work3 wk = decode3<FUSED ? 2 : 1>(sc, t);  // uniform: every index below in SGPRs
   while (wk.phase == 1) {
     unsigned tnext = 0;
     if (tid == 0) tnext = atomicAdd(ctr, 1u);
@@ -920,9 +924,9 @@ EKS_DEV unsigned k3_bwd_run(const SmoothArgs &a, const Plan3 &p, const Sched3 &s
 #pragma unroll
       for (int u = 0; u < R; ++u) ms[u] = 0.0;
       if (cc + 1 < p.NCc) {
-        const unsigned *fl = flags + grp;
+        const unsigned *fl = flags + grp * p.NCc;  // group-major
         long long j = cc + 1;
-        if (!inc_ready(fl + j * p.ng, a.wait_ticks)) {
+        if (!inc_ready(fl + j, a.wait_ticks)) {
           if (cc > 0) {
             if (lane_ok) {
               double *mp0 = agg2;
@@ -939,9 +943,9 @@ EKS_DEV unsigned k3_bwd_run(const SmoothArgs &a, const Plan3 &p, const Sched3 &s
                 for (int k = 0; k < MP; ++k)
                   st_wt(&pl(mp0, base + v * MP + k, B, b), shM[v - 1][k][l]);
             }
-            publish_flag(flags + cc * p.ng + grp, l, kAggReady);
+            publish_flag(flags + grp * p.NCc + cc, l, kAggReady);
           }
-          j = look_back(fl, j, p.ng, +1, p.NCc, a.wait_ticks, okc);
+          j = look_back(fl, j, 1, +1, p.NCc, a.wait_ticks, okc);
         }
         if (lane_ok) {
 #pragma unroll
@@ -985,7 +989,7 @@ EKS_DEV unsigned k3_bwd_run(const SmoothArgs &a, const Plan3 &p, const Sched3 &s
         if (lane_ok)
 #pragma unroll
           for (int u = 0; u < R; ++u) st_wt(&pl(inc, cc * R + u, B, b), x[u]);
-        publish_flag(flags + cc * p.ng + grp, l, kIncReady);
+        publish_flag(flags + grp * p.NCc + cc, l, kIncReady);
       }
     }
     __syncthreads();
@@ -1086,7 +1090,7 @@ EKS_DEV unsigned k3_bwd_run(const SmoothArgs &a, const Plan3 &p, const Sched3 &s
     if (tid == 0) tk[(it + 1) & 1] = tnext;
     __syncthreads();  // LDS free for the next unit, its ticket visible
     t = __builtin_amdgcn_readfirstlane(tk[(it + 1) & 1]);
-    wk = decode3(sc, t);
+    wk = decode3<FUSED ? 2 : 1>(sc, t);
     ++it;
   }
   return t;
@@ -1118,7 +1122,7 @@ __global__ __launch_bounds__(64 * kWV) void k3_fused(SmoothArgs a, Plan3 p, Sche
   unsigned t = __builtin_amdgcn_readfirstlane(tk[0]);
   int it = 0;
   while (true) {
-    const Work3 wk = decode3(sc, t);
+    const Work3 wk = decode3<2>(sc, t);
     if (wk.phase == 0)
       t = k3_fwd_run<R, N, E, T, AI, CI, true, FWD_NT>(a, p, sc, t, lds, tk, ctr, it);
     else if (wk.phase == 1)
