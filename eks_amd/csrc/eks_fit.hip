@@ -572,6 +572,14 @@ __global__ __launch_bounds__(256) void k_sel_cand(const double *__restrict__ wor
   uint64_t *ck = ckey + b * TT;
   unsigned *ci = cidx + b * TT;
   unsigned long long above = ~0ull;
+  // the segment's bin keys are staged in LDS and appended with ONE global
+  // atomic per block (per-wave atomics on the row's counter serialised: ~400
+  // per row at config 2)
+  __shared__ uint64_t sk[kSegKeys];
+  __shared__ unsigned sidx[kSegKeys];
+  __shared__ unsigned scount, sbase;
+  if (threadIdx.x == 0) scount = 0;
+  __syncthreads();
   // whole waves per 64-key word: k0 is a multiple of 64 and every wave of the
   // loop runs the same iterations (the index test is on the wave's last lane)
   for (long long i0 = k0 + (threadIdx.x & ~63); i0 < k1; i0 += 256) {
@@ -590,19 +598,34 @@ __global__ __launch_bounds__(256) void k_sel_cand(const double *__restrict__ wor
     const int lane = threadIdx.x & 63;
     const unsigned below = (unsigned)__popcll(m & ((1ull << lane) - 1));
     unsigned base = 0;
-    if (lane == __ffsll((long long)m) - 1) base = atomicAdd(&row.ncand, (unsigned)__popcll(m));
+    if (lane == __ffsll((long long)m) - 1) base = atomicAdd(&scount, (unsigned)__popcll(m));
     base = __shfl(base, __ffsll((long long)m) - 1, 64);
     if (in) {
-      ck[base + below] = x;
-      ci[base + below] = (unsigned)i;
+      sk[base + below] = x;
+      sidx[base + below] = (unsigned)i;
     }
   }
-  if (!nan && above != ~0ull) atomicMin(&row.above, above);
+  // the least key above the bin: wave minimum, then one atomic per wave
+  for (int o = 32; o >= 1; o >>= 1) {
+    const unsigned long long other = __shfl_xor(above, o, 64);
+    above = other < above ? other : above;
+  }
+  if (!nan && (threadIdx.x & 63) == 0 && above != ~0ull) atomicMin(&row.above, above);
+  __syncthreads();
+  const unsigned cnt = scount;
+  if (cnt == 0) return;
+  if (threadIdx.x == 0) sbase = atomicAdd(&row.ncand, cnt);
+  __syncthreads();
+  const unsigned base = sbase;
+  for (unsigned k = threadIdx.x; k < cnt; k += 256) {
+    ck[base + k] = sk[k];
+    ci[base + k] = sidx[k];
+  }
 }
 
-// candidates of the split selection held in LDS (128 KB: the kernel runs one
+// candidates of the split selection held in LDS (156 KB: the kernel runs one
 // 1024-thread block per row, few rows)
-constexpr int kCandBig = 16384;
+constexpr int kCandBig = 19968;  // 156 KB
 
 template <int BLK>
 __global__ __launch_bounds__(BLK) void k_sel_final(const double *__restrict__ worst, long long TT,
@@ -1272,10 +1295,14 @@ extern "C" int eks_fit(const void *obs, int obs_dtype, int64_t B, int64_t T, int
               hipSuccess)
             return set_err(EKS_ERR_HIP, "eks_fit: hipMemsetAsync failed");
           const unsigned gs = (unsigned)(B * G);
+          prof_mark(s, "k_sel_hist");
           hipLaunchKernelGGL(k_sel_hist, dim3(gs), dim3(256), 0, s, worst, T, G, ghist, rows);
+          prof_mark(s, "k_sel_bin");
           hipLaunchKernelGGL(k_sel_bin, dim3((unsigned)B), dim3(256), 0, s, ghist, lo, rows);
+          prof_mark(s, "k_sel_cand");
           hipLaunchKernelGGL(k_sel_cand, dim3(gs), dim3(256), 0, s, worst, T, G, rows, ckey, cidx,
                              yev ? kept : nullptr, W);
+          prof_mark(s, "k_sel_final");
           hipLaunchKernelGGL(k_sel_final<1024>, dim3((unsigned)B), dim3(1024), 0, s, worst, T,
                              hi - lo, g, rows, ckey, cidx, thr, yev ? kept : nullptr, W);
         } else if (T >= 65536) {

@@ -107,10 +107,10 @@ def test_mask_long_rows_whole_row_pass(torch):
     _vs_host(st, p, 25.0)
 
 
-@pytest.mark.parametrize("T,big", [(40000, 4096), (160000, 16384)])
+@pytest.mark.parametrize("T,big", [(40000, 4096), (160000, 19968)])
 def test_mask_bin_larger_than_lds(torch, T, big):
     """No outliers and long rows: the threshold's top-digit bin holds more
-    frames than the LDS candidate buffer (3 072 for one block per row, 16 384
+    frames than the LDS candidate buffer (3 072 for one block per row, 19 968
     for the split selection's final block), so the select runs over the
     global row / candidate buffer and the mask comes from the whole-row pass."""
     from eks_amd import synthetic
