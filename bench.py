@@ -82,6 +82,8 @@ def parse():
     ap.add_argument("--a3-mode", type=int, default=0,
                     help="tuning: algo 3's launch form (eks_debug_set EKS_DBG_A3_MODE: 0 default, "
                          "1 two launches, 2 one launch)")
+    ap.add_argument("--a3-lb", type=int, default=0,
+                    help="tuning: algo 3's backward look-back (EKS_DBG_A3_LB: 0 auto, 1 off, 2 on)")
     ap.add_argument("--scaling", choices=["strong", "weak"], default="strong",
                     help="config 4: strong = the video batch is split over ranks; weak = "
                          "every rank smooths --videos videos")
@@ -612,6 +614,8 @@ def main():
     t_setup = time.perf_counter()
     if a.a3_mode:
         _lib.debug_set(_lib.EKS_DBG_A3_MODE, a.a3_mode)
+    if a.a3_lb:
+        _lib.debug_set(_lib.EKS_DBG_A3_LB, a.a3_lb)
     if a.config in (2, 4):
         w = workload_singleview(torch, a, dev, rank, world, a.config)
     elif a.config == 3:

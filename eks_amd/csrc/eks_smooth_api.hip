@@ -43,6 +43,7 @@ int launch_rt(const SmoothArgs &a);
 long long g_wait_ticks = kDefaultWaitTicks;
 long long g_a3_slice_bytes = 0;
 long long g_a3_mode = 0;
+long long g_a3_lb = 0;
 extern long long g_fit_select;  // eks_fit.hip
 }
 
@@ -194,6 +195,11 @@ int64_t eks_debug_set(int key, int64_t value) {
     case EKS_DBG_A3_MODE: {
       const long long prev = g_a3_mode;
       g_a3_mode = value > 0 ? value : 0;
+      return prev;
+    }
+    case EKS_DBG_A3_LB: {
+      const long long prev = g_a3_lb;
+      g_a3_lb = value == 1 || value == 2 ? value : 0;
       return prev;
     }
     case EKS_DBG_FIT_SELECT: {

@@ -53,6 +53,7 @@ namespace eks {
 extern long long g_wait_ticks;      // chain wait bound (wall_clock64 ticks), < 0: forced timeouts
 extern long long g_a3_slice_bytes;  // algo-3 member offset span per slice (0: 4 GB)
 extern long long g_a3_mode;         // algo-3 launch form (two_pass.hpp a3_fused_groups)
+extern long long g_a3_lb;           // k3_bwd look-back instantiation (two_pass.hpp a3_bwd_lookback)
 
 struct SmoothArgs {
   const void *obs;

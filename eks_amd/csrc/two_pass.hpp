@@ -764,7 +764,12 @@ constexpr int bwd_lds_doubles() {
 // The k3_bwd units of consecutive tickets from t on (a run ends at the first
 // ticket that is not a k3_bwd unit, which is returned).  FUSED: each wave
 // first waits for the k3_fwd unit that stored its fine chunk's start state.
-template <int R, int N, int E, typename T, int AI, int CI, bool NLL, bool FUSED>
+// LB: the backward chain's look-back (publish the unit's maps, walk, fold).
+// Its code costs the hot loop SGPRs (spills: 21 -> 153 v_readlane in the
+// ISA, k3_bwd 1.94 -> 2.16 ms at config 4) while it only pays where few
+// groups share the chip (the 8-GPU shard: 0.365 -> 0.348 ms), so it is a
+// separate instantiation, launched for small batches (a3_bwd_lookback).
+template <int R, int N, int E, typename T, int AI, int CI, bool NLL, bool FUSED, bool LB = true>
 EKS_DEV unsigned k3_bwd_run(const SmoothArgs &a, const Plan3 &p, const Sched3 &sc, unsigned t,
                             double *lds, unsigned *tk, unsigned *ctr, int &it) {
   constexpr int KS = R + Sym<R>::len, MP = R * R + R;
@@ -926,7 +931,9 @@ EKS_DEV unsigned k3_bwd_run(const SmoothArgs &a, const Plan3 &p, const Sched3 &s
       if (cc + 1 < p.NCc) {
         const unsigned *fl = flags + grp * p.NCc;  // group-major
         long long j = cc + 1;
-        if (!inc_ready(fl + j, a.wait_ticks)) {
+        if (!LB) {
+          if (!wait_flag(fl + j, a.wait_ticks, kIncReady)) okc = false;
+        } else if (!inc_ready(fl + j, a.wait_ticks)) {
           if (cc > 0) {
             if (lane_ok) {
               double *mp0 = agg2;
@@ -1096,7 +1103,7 @@ EKS_DEV unsigned k3_bwd_run(const SmoothArgs &a, const Plan3 &p, const Sched3 &s
   return t;
 }
 
-template <int R, int N, int E, typename T, int AI, int CI, bool NLL>
+template <int R, int N, int E, typename T, int AI, int CI, bool NLL, bool LB>
 __global__ __launch_bounds__(64 * kWV) void k3_bwd(SmoothArgs a, Plan3 p, Sched3 sc) {
   __shared__ double lds[bwd_lds_doubles<R, N>()];
   __shared__ unsigned tk[2];
@@ -1104,7 +1111,7 @@ __global__ __launch_bounds__(64 * kWV) void k3_bwd(SmoothArgs a, Plan3 p, Sched3
   if (threadIdx.x == 0) tk[0] = atomicAdd(ctr, 1u);
   __syncthreads();
   int it = 0;
-  k3_bwd_run<R, N, E, T, AI, CI, NLL, false>(a, p, sc, __builtin_amdgcn_readfirstlane(tk[0]), lds,
+  k3_bwd_run<R, N, E, T, AI, CI, NLL, false, LB>(a, p, sc, __builtin_amdgcn_readfirstlane(tk[0]), lds,
                                              tk, ctr, it);
 }
 
@@ -1157,6 +1164,16 @@ inline long long a3_fused_groups(const Plan3 &p) {
   return g_a3_mode >= 2 ? p.ng : 0;
 }
 
+// k3_bwd's look-back instantiation (LB): for batches of at most kLbGroups
+// 64-trajectory groups, where several time chunks of a group are resident at
+// once (eks_debug_set(EKS_DBG_A3_LB): 1 never, 2 always, 0 this rule)
+constexpr long long kLbGroups = 96;
+inline bool a3_bwd_lookback(const Plan3 &p) {
+  if (g_a3_lb == 1) return false;
+  if (g_a3_lb == 2) return true;
+  return p.ng <= kLbGroups;
+}
+
 // host: the launches of one algo-3 call
 template <int R, int N, int AI, int CI>
 int launch_algo3_one(const SmoothArgs &a) {
@@ -1201,14 +1218,29 @@ int launch_algo3_one(const SmoothArgs &a) {
       if ((rc = check_launch("k3_fwd"))) return rc;
       prof_mark(a.stream, "k3_bwd");
       const Sched3 sb = make_sched3(p, 1, 0);
-      if (a.nll)
-        hipLaunchKernelGGL((k3_bwd<R, N, EE, Tp, AI, CI, true>),
-                           dim3(persistent_grid<k3_bwd<R, N, EE, Tp, AI, CI, true>>(p.units)),
-                           dim3(64 * kWV), 0, a.stream, a, p, sb);
-      else
-        hipLaunchKernelGGL((k3_bwd<R, N, EE, Tp, AI, CI, false>),
-                           dim3(persistent_grid<k3_bwd<R, N, EE, Tp, AI, CI, false>>(p.units)),
-                           dim3(64 * kWV), 0, a.stream, a, p, sb);
+      // the look-back instantiation only for small batches of the
+      // single-view shape (kCanFuse: the throughput shape)
+      bool lb = false;
+      if constexpr (kCanFuse) lb = a3_bwd_lookback(p);
+      if (a.nll) {
+        if (lb)
+          hipLaunchKernelGGL((k3_bwd<R, N, EE, Tp, AI, CI, true, true>),
+                             dim3(persistent_grid<k3_bwd<R, N, EE, Tp, AI, CI, true, true>>(p.units)),
+                             dim3(64 * kWV), 0, a.stream, a, p, sb);
+        else
+          hipLaunchKernelGGL((k3_bwd<R, N, EE, Tp, AI, CI, true, false>),
+                             dim3(persistent_grid<k3_bwd<R, N, EE, Tp, AI, CI, true, false>>(p.units)),
+                             dim3(64 * kWV), 0, a.stream, a, p, sb);
+      } else {
+        if (lb)
+          hipLaunchKernelGGL((k3_bwd<R, N, EE, Tp, AI, CI, false, true>),
+                             dim3(persistent_grid<k3_bwd<R, N, EE, Tp, AI, CI, false, true>>(p.units)),
+                             dim3(64 * kWV), 0, a.stream, a, p, sb);
+        else
+          hipLaunchKernelGGL((k3_bwd<R, N, EE, Tp, AI, CI, false, false>),
+                             dim3(persistent_grid<k3_bwd<R, N, EE, Tp, AI, CI, false, false>>(p.units)),
+                             dim3(64 * kWV), 0, a.stream, a, p, sb);
+      }
       if ((rc = check_launch("k3_bwd"))) return rc;
     }
     if (a.nll) {

@@ -330,9 +330,12 @@ int eks_interp1d(const double *x, int64_t nx, const double *y, int64_t ncol, int
  *                          launches), 1 = two launches (forward pass,
  *                          backward pass), 2 = one persistent launch, all
  *                          forward units first.  Results are bit-identical.
+ *   EKS_DBG_A3_LB          algo 3's backward look-back: 0 = automatic (batches
+ *                          of at most 96 64-trajectory groups), 1 = never,
+ *                          2 = always.  Results are bit-identical.
  */
 enum { EKS_DBG_WAIT_US = 1, EKS_DBG_A3_SLICE_BYTES = 2, EKS_DBG_FIT_SELECT = 3,
-       EKS_DBG_A3_MODE = 4 };
+       EKS_DBG_A3_MODE = 4, EKS_DBG_A3_LB = 5 };
 int64_t eks_debug_set(int key, int64_t value);
 
 /*
