@@ -25,6 +25,7 @@ EKS_YEV32, EKS_YEV64 = 2, 3
 EKS_MEDIAN, EKS_MEAN = 0, 1
 EKS_DBG_WAIT_US, EKS_DBG_A3_SLICE_BYTES, EKS_DBG_FIT_SELECT, EKS_DBG_A3_MODE = 1, 2, 3, 4
 EKS_DBG_A3_LB = 5
+EKS_DBG_RT_FORM = 6
 
 _p = C.c_void_p
 _i64 = C.c_int64

@@ -39,11 +39,11 @@ bool use_rt(int r, int n, int algo) {
 }  // namespace
 
 namespace eks {
-int launch_rt(const SmoothArgs &a);
 long long g_wait_ticks = kDefaultWaitTicks;
 long long g_a3_slice_bytes = 0;
 long long g_a3_mode = 0;
 long long g_a3_lb = 0;
+long long g_rt_form = 0;
 extern long long g_fit_select;  // eks_fit.hip
 }
 
@@ -64,7 +64,7 @@ int eks_smooth_algo(int64_t B, int64_t T, int n, int r, int E, int algo) {
 size_t eks_smooth_workspace_bytes(int64_t B, int64_t T, int n, int r, int E, int algo) {
   (void)E;
   if (B <= 0 || T <= 0 || r < 1 || n < 1) return 0;
-  if (use_rt(r, n, algo)) return seq_workspace_bytes(B, T, r);
+  if (use_rt(r, n, algo)) return rt_workspace_bytes(B, T, n, r);
   const int al = pick_algo(B, T, n, r, E, algo);
   if (al == 1) return seq_workspace_bytes(B, T, r);
   // smoothing calls of few trajectories use shorter chunks than filter-only ones
@@ -200,6 +200,11 @@ int64_t eks_debug_set(int key, int64_t value) {
     case EKS_DBG_A3_LB: {
       const long long prev = g_a3_lb;
       g_a3_lb = value == 1 || value == 2 ? value : 0;
+      return prev;
+    }
+    case EKS_DBG_RT_FORM: {
+      const long long prev = g_rt_form;
+      g_rt_form = value == 1 || value == 2 ? value : 0;
       return prev;
     }
     case EKS_DBG_FIT_SELECT: {

@@ -558,10 +558,9 @@ EKS_DEV void absorb_row(Elem<3> &E, double y, double r, bool &ok, NllAcc *acc) {
 //   -log p(y_{s..e-1} | x) = K + 1/2 x^T Jb x - eta^T x,
 //   K = 1/2 sum_i (log 2 pi + log s_i + e0_i^2 / s_i)   (acc.value)
 // which elem_nll_share turns into the chunk's NLL share.
-template <int R, int N, int AI, int CI>
-EKS_DEV void elem_absorb(Elem<R> &E, const double (&A)[R][R], const double (&Q)[R][R],
-                         const double (&C)[N][R], const double (&y)[N], const double (&rv)[N],
-                         bool &ok, NllAcc *acc = nullptr) {
+// the predict half: E <- (A Ab, A bb, A Cb A^T + Q)
+template <int R, int AI>
+EKS_DEV void elem_predict(Elem<R> &E, const double (&A)[R][R], const double (&Q)[R][R]) {
   if constexpr (AI == kAId) {
 #pragma unroll
     for (int i = 0; i < R; ++i)
@@ -608,6 +607,38 @@ EKS_DEV void elem_absorb(Elem<R> &E, const double (&A)[R][R], const double (&Q)[
 #pragma unroll
       for (int j = 0; j < i; ++j) E.Cb[i][j] = E.Cb[j][i];
   }
+}
+
+// one scalar observation y ~ N(c x, rv) with a general row c
+template <int R>
+EKS_DEV void absorb_gen_row(Elem<R> &E, const double (&c)[R], double y, double rv, bool &ok,
+                            NllAcc *acc) {
+  double v[R], g[R];
+#pragma unroll
+  for (int a = 0; a < R; ++a) {
+    double tv = 0.0, tg = 0.0;
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      tv = fma(E.Cb[a][k], c[k], tv);
+      tg = fma(E.Ab[k][a], c[k], tg);
+    }
+    v[a] = tv;
+    g[a] = tg;
+  }
+  double s = rv, hb = 0.0;
+#pragma unroll
+  for (int k = 0; k < R; ++k) {
+    s = fma(c[k], v[k], s);
+    hb = fma(c[k], E.bb[k], hb);
+  }
+  absorb_scalar<R>(E, v, g, s, hb, y, ok, acc);
+}
+
+template <int R, int N, int AI, int CI>
+EKS_DEV void elem_absorb(Elem<R> &E, const double (&A)[R][R], const double (&Q)[R][R],
+                         const double (&C)[N][R], const double (&y)[N], const double (&rv)[N],
+                         bool &ok, NllAcc *acc = nullptr) {
+  elem_predict<R, AI>(E, A, Q);
   if constexpr (CI == kCPupil) {
     static_assert(R == 3 && N == 8, "the pupil model is r = 3, n = 8");
     double ya, ra, yb, rb;
@@ -624,36 +655,17 @@ EKS_DEV void elem_absorb(Elem<R> &E, const double (&A)[R][R], const double (&Q)[
   }
 #pragma unroll
   for (int i = 0; i < N; ++i) {
-    double v[R], g[R], s, hb;
     if constexpr (CI == kCId) {
+      double v[R], g[R];
 #pragma unroll
       for (int a = 0; a < R; ++a) {
         v[a] = E.Cb[a][i];
         g[a] = E.Ab[i][a];
       }
-      s = v[i] + rv[i];
-      hb = E.bb[i];
+      absorb_scalar<R>(E, v, g, v[i] + rv[i], E.bb[i], y[i], ok, acc);
     } else {
-#pragma unroll
-      for (int a = 0; a < R; ++a) {
-        double tv = 0.0, tg = 0.0;
-#pragma unroll
-        for (int k = 0; k < R; ++k) {
-          tv = fma(E.Cb[a][k], C[i][k], tv);
-          tg = fma(E.Ab[k][a], C[i][k], tg);
-        }
-        v[a] = tv;
-        g[a] = tg;
-      }
-      s = rv[i];
-      hb = 0.0;
-#pragma unroll
-      for (int k = 0; k < R; ++k) {
-        s = fma(C[i][k], v[k], s);
-        hb = fma(C[i][k], E.bb[k], hb);
-      }
+      absorb_gen_row<R>(E, C[i], y[i], rv[i], ok, acc);
     }
-    absorb_scalar<R>(E, v, g, s, hb, y[i], ok, acc);
   }
   if (acc) acc->renorm();
 }

@@ -53,6 +53,7 @@ namespace eks {
 extern long long g_wait_ticks;      // chain wait bound (wall_clock64 ticks), < 0: forced timeouts
 extern long long g_a3_slice_bytes;  // algo-3 member offset span per slice (0: 4 GB)
 extern long long g_a3_mode;         // algo-3 launch form (two_pass.hpp a3_fused_groups)
+extern long long g_rt_form;         // runtime-n smoother form (eks_shape_rt.hip rt_chunked)
 extern long long g_a3_lb;           // k3_bwd look-back instantiation (two_pass.hpp a3_bwd_lookback)
 
 struct SmoothArgs {
@@ -258,7 +259,10 @@ struct ChunkPlan {
 
 inline size_t align256(size_t x) { return (x + 255) / 256 * 256; }
 
-inline ChunkPlan make_plan(long long B, long long T, int r, int n, long long L) {
+// force_jd: the (J, d) planes whatever jd_shape says (the runtime-n pipeline
+// always runs K5 from them)
+inline ChunkPlan make_plan(long long B, long long T, int r, int n, long long L,
+                           bool force_jd = false) {
   ChunkPlan p;
   p.LS = sub_len(r, n);
   p.L = L;
@@ -279,7 +283,7 @@ inline ChunkPlan make_plan(long long B, long long T, int r, int n, long long L) 
   p.nllp_off = take((size_t)p.NC * Bz * 8);
   p.msend_off = take((size_t)p.NC * r * Bz * 8);
   p.ckpt_off = take((size_t)p.NC * p.NSUB * state_len(r) * Bz * 8);
-  if (jd_shape(B, r, n)) p.jd_off = take((size_t)T * (r * r + r) * Bz * 8);
+  if (force_jd || jd_shape(B, r, n)) p.jd_off = take((size_t)T * (r * r + r) * Bz * 8);
   if (p.NC > wave_scan_chunks()) {
     // blocks per trajectory: few lanes in all -> ~1 chunk per thread (the
     // scan is latency bound); many -> q chunks per thread so the chip holds
@@ -315,6 +319,12 @@ inline ChunkPlan make_plan(long long B, long long T, int r, int n, long long L) 
 
 inline size_t seq_workspace_bytes(long long B, long long T, int r) {
   return (size_t)B * (size_t)T * (size_t)state_len(r) * 8;
+}
+
+// parameter row stride; N = 0: the runtime-n kernels (eks_shape_rt.hip)
+template <int R, int N>
+EKS_DEV long long param_stride(int n) {
+  return N > 0 ? (long long)ParamLayout<R, N>::len : (long long)R + 3LL * R * R + (long long)n * (R + 1);
 }
 
 // model of one trajectory in registers
@@ -880,7 +890,7 @@ __global__ __launch_bounds__(64) void k_c2_fscan(SmoothArgs a, ChunkPlan p) {
   bool ok = true;
   if (a.t_base == 0) {
     using L = ParamLayout<R, N>;
-    const double *pp = a.params + b * L::len;
+    const double *pp = a.params + b * param_stride<R, N>(a.n);
     load_vec<R>(pp + L::m0, m);
     load_mat<R, R>(pp + L::S0, P);
     store_state<R>(cst + b, B, m, P);  // chunk 0 starts from the prior
@@ -1102,7 +1112,7 @@ __global__ __launch_bounds__(256) void k_c2_fscan_g(SmoothArgs a, ChunkPlan p) {
     long long c = c0;
     if (first) {
       using L = ParamLayout<R, N>;
-      const double *pp = a.params + b * L::len;
+      const double *pp = a.params + b * param_stride<R, N>(a.n);
       load_vec<R>(pp + L::m0, m);
       load_mat<R, R>(pp + L::S0, P);
       store_state<R>(cst + b, B, m, P);  // chunk 0 starts from the prior
@@ -2235,6 +2245,10 @@ int launch_seg_combine(int kind, long long B, int nseg, int self, const double *
                      self, in, out, status);
   return check_launch("k_seg_combine");
 }
+
+// the runtime-n smoother (eks_shape_rt.hip)
+int launch_rt(const SmoothArgs &a);
+size_t rt_workspace_bytes(long long B, long long T, int n, int r);
 
 // per-shape entry points (defined in eks_shape_*.hip)
 int launch_22(const SmoothArgs &a, int algo, long long L);

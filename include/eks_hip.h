@@ -178,14 +178,15 @@ int64_t eks_param_len(int n, int r);
  *            3 = time-parallel, two passes over the members (chunk-level RTS
  *            maps; smoothing only: a filter-only call runs algo 2; needs
  *            E in 3..5 or y / ev planes, else algo 2),
- *            4 = the runtime-n sequential kernel (any n <= 64, r = 2 or 3,
- *            member inputs): what every (r, n) without compiled kernels runs
- *            -- (2, 2) and (3, 4|6|8) are compiled; e.g. the multi-camera
- *            model with V > 4 cameras, n = 2V (the reference accepts any V:
+ *            4 = the runtime-n kernels (any n <= 64, r = 2 or 3, member
+ *            inputs): what every (r, n) without compiled kernels runs --
+ *            (2, 2) and (3, 4|6|8) are compiled; e.g. the multi-camera model
+ *            with V > 4 cameras, n = 2V (the reference accepts any V:
  *            eks/multiview_pca_smoother.py:641-666).  eks_smooth_algo
- *            reports 4 for those shapes.  One GPU lane per trajectory,
- *            sequential in time: throughput needs many trajectories (a
- *            single long trajectory runs on one lane).
+ *            reports 4 for those shapes.  Many trajectories: one GPU lane
+ *            per trajectory, sequential in time; few long ones: algo 2's
+ *            time-parallel chunk scan with the n observation rows streamed
+ *            one at a time (EKS_DBG_RT_FORM below).
  *   status   (B) int32, REQUIRED; zeroed by the call, then bit flags as above.
  */
 size_t eks_smooth_workspace_bytes(int64_t B, int64_t T, int n, int r, int E, int algo);
@@ -333,9 +334,14 @@ int eks_interp1d(const double *x, int64_t nx, const double *y, int64_t ncol, int
  *   EKS_DBG_A3_LB          algo 3's backward look-back: 0 = automatic (batches
  *                          of at most 96 64-trajectory groups), 1 = never,
  *                          2 = always.  Results are bit-identical.
+ *   EKS_DBG_RT_FORM        the runtime-n smoother (algo 4): 0 = automatic
+ *                          (time-parallel when the trajectories alone do not
+ *                          fill the GPU), 1 = one lane per trajectory, 2 =
+ *                          time-parallel.  Results agree to rounding; set it
+ *                          before eks_smooth_workspace_bytes.
  */
 enum { EKS_DBG_WAIT_US = 1, EKS_DBG_A3_SLICE_BYTES = 2, EKS_DBG_FIT_SELECT = 3,
-       EKS_DBG_A3_MODE = 4, EKS_DBG_A3_LB = 5 };
+       EKS_DBG_A3_MODE = 4, EKS_DBG_A3_LB = 5, EKS_DBG_RT_FORM = 6 };
 int64_t eks_debug_set(int key, int64_t value);
 
 /*

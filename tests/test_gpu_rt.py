@@ -35,10 +35,19 @@ def test_multicam_wrapper_many_cameras_vs_oracle(torch, V, T):
     assert np.abs(got - ref).max() < 1e-5
 
 
+@pytest.fixture
+def rt_form():
+    """eks_debug_set(EKS_DBG_RT_FORM, v) for one test, reset afterwards."""
+    from eks_amd import _lib
+    yield lambda v: _lib.debug_set(_lib.EKS_DBG_RT_FORM, v)
+    _lib.debug_set(_lib.EKS_DBG_RT_FORM, 0)
+
+
 @pytest.mark.parametrize("r,n,E", [(2, 2, 5), (2, 2, 7), (3, 8, 5), (3, 6, 4)])
-def test_runtime_n_kernel_equals_compiled(torch, r, n, E):
+def test_runtime_n_kernel_equals_compiled(torch, rt_form, r, n, E):
     from eks_amd import batch, synthetic
     from oracle import eks_oracle as O
+    rt_form(1)  # the one-lane-per-trajectory form: the compiled kernels' update order
     rng = np.random.default_rng(r * 100 + n * 10 + E)
     B, T = 70, 500
     if r == 2:
@@ -91,3 +100,48 @@ def test_runtime_n_nll_and_filter_only(torch):
     assert np.abs(res["out"].cpu().numpy() - np.stack(refs)).max() < 1e-5
     np.testing.assert_allclose(res["nll"].cpu().numpy(), nlls, rtol=1e-9)
     np.testing.assert_allclose(batch.nll(d, params, n=n, r=3).cpu().numpy(), nlls, rtol=1e-9)
+
+
+@pytest.mark.parametrize("r,n,B,T", [(3, 10, 3, 6000), (3, 12, 17, 3000), (3, 16, 2, 20000),
+                                     (2, 2, 5, 4000), (3, 10, 1, 37)])
+def test_runtime_n_time_parallel_equals_sequential(torch, rt_form, r, n, B, T):
+    """The time-parallel runtime-n form (algo 2's chunk scans with the rows
+    streamed) against the one-lane form: outputs, latent means and NLL
+    (smoothing and filter-only calls), the tolerances of the compiled
+    time-parallel algorithms (tests/test_gpu_configs.py PX_ALGO, NLL_RTOL);
+    T = 20000 at B = 2 runs the wave-parallel chunk scans."""
+    from eks_amd import batch, synthetic
+    from oracle import eks_oracle as O
+    rng = np.random.default_rng(n * 1000 + B)
+    E = 5
+    if r == 2:
+        st = synthetic.singleview_obs(rng, E, T, K=B).transpose(2, 0, 1, 3)
+    else:
+        st = synthetic.multiview_obs(rng, n // 2, E, T, K=B).transpose(2, 0, 1, 3)
+    models = []
+    for b in range(B):
+        preds, ev = O.ensemble_array(st[b].astype(np.float64))
+        models.append(O.singleview_params(preds, ev, 0.01, 25) if r == 2 else
+                      O.multicam_params(preds, ev, 0.01, 25))
+    stk = lambda k: np.stack([m[k] for m in models])  # noqa: E731
+    params = batch.pack_params(stk("m0"), stk("S0"), stk("A"), stk("Q"), stk("C"), stk("means"))
+    d = batch.make_time_major(st, dtype=np.float32)
+    res = {}
+    for form in (1, 2):
+        rt_form(form)
+        res[form] = batch.smooth(d, params, n=n, r=r, algo=4, flags=0, want_nll=True,
+                                 want_ms=True, check=True)
+        res[form]["nll_only"] = batch.nll(d, params, n=n, r=r, algo=4)
+    a, b_ = res[1], res[2]
+    assert float((a["out"] - b_["out"]).abs().max()) < 1e-8
+    assert float((a["ms"] - b_["ms"]).abs().max()) < 1e-8
+    for k in ("nll", "nll_only"):
+        rel = float(((a[k] - b_[k]) / a[k].abs()).abs().max())
+        assert rel < 1e-10, (k, rel)
+    # and the oracle on the first trajectory
+    p = models[0]
+    ev = O.ensemble_array(st[0].astype(np.float64))[1]
+    mf, Vf, S = O.filtering_pass(p["y"], p["m0"], p["S0"], p["C"], np.eye(n), p["A"], p["Q"], ev)
+    ms, _, _ = O.smooth_backward(p["y"], mf, Vf, S, p["A"])
+    ref = ms @ p["C"].T + p["means"]
+    assert np.abs(b_["out"][0].cpu().numpy() - ref).max() < 1e-5
