@@ -40,7 +40,9 @@ def test_limits_and_sizes():
     # shapes without compiled kernels (five cameras: n = 10) run the runtime-n kernel
     assert lib.eks_smooth_algo(17, 50000, 10, 3, 5, 0) == 4
     assert lib.eks_smooth_algo(17, 50000, 8, 3, 5, 4) == 4
-    assert lib.eks_smooth_workspace_bytes(17, 1000, 10, 3, 5, 0) == 17 * 1000 * 9 * 8
+    # ... sequential for many trajectories, time-parallel (chunk planes) for few
+    assert lib.eks_smooth_workspace_bytes(1 << 20, 100, 10, 3, 5, 0) == (1 << 20) * 100 * 9 * 8
+    assert lib.eks_smooth_workspace_bytes(17, 1000, 10, 3, 5, 0) > 17 * 1000 * 10 * 16
     assert lib.eks_smooth_workspace_bytes(17, 100000, 2, 2, 5, 2) >= 17 * 100000 * 2 * 16
 
 
