@@ -726,6 +726,15 @@ EKS_DEV constexpr int tri(int i, int j) {  // i <= j
   return i * N - i * (i - 1) / 2 + (j - i);
 }
 
+// the same layout for a runtime n (the wide fit; k_fit_merge<0>)
+struct CsRt {
+  int n, kTri, cnt, mean, M, npair, dmean, dM, first, last, kLen;
+  EKS_DEV explicit CsRt(int n_)
+      : n(n_), kTri(n_ * (n_ + 1) / 2), cnt(0), mean(1), M(1 + n_), npair(1 + n_ + kTri),
+        dmean(npair + 1), dM(dmean + n_), first(dM + kTri), last(first + n_), kLen(last + n_) {}
+  EKS_DEV int tri(int i, int j) const { return i * n - i * (i - 1) / 2 + (j - i); }
+};
+
 // the sums of a frame range, merged as  L (+) R  (R the later frames)
 template <int N>
 struct Partial {
@@ -924,21 +933,21 @@ __global__ __launch_bounds__(256) void k_fit_accum(const T *__restrict__ obs, Fi
 // there is no cross-thread dependence.  The F partials' loads are issued
 // kMergeUnroll at a time ahead of the (sequential, fixed-order) additions.
 constexpr int kMergeUnroll = 4;
-template <int N>
+template <int N>  // N = 0: n = nrt (the wide fit)
 __global__ __launch_bounds__(256) void k_fit_merge(long long B, int nc_in, int F,
                                                    const double *__restrict__ in,
-                                                   double *__restrict__ out) {
-  using CS = ChunkStats<N>;
+                                                   double *__restrict__ out, int nrt) {
+  const CsRt CS(N > 0 ? N : nrt);  // compile-time constants for N > 0
   const int nc_out = (nc_in + F - 1) / F;
   const long long gid = blockIdx.x * (long long)blockDim.x + threadIdx.x;
-  const long long total = B * nc_out * CS::kTri;
+  const long long total = B * nc_out * CS.kTri;
   if (gid >= total) return;
-  const int e = (int)(gid % CS::kTri);
-  const long long bg = gid / CS::kTri;
+  const int e = (int)(gid % CS.kTri);
+  const long long bg = gid / CS.kTri;
   const long long b = bg % B, g = bg / B;
   int i = 0;
-  while (tri<N>(i, N - 1) < e) ++i;  // element e = (i, j), i <= j
-  const int j = i + (e - tri<N>(i, i));
+  while (CS.tri(i, CS.n - 1) < e) ++i;  // element e = (i, j), i <= j
+  const int j = i + (e - CS.tri(i, i));
   double n = 0.0, si = 0.0, s2 = 0.0, np_ = 0.0, di = 0.0, dj = 0.0, d2 = 0.0;
   double fi = 0.0, li = 0.0, lj = 0.0;
   bool have = false;
@@ -948,18 +957,18 @@ __global__ __launch_bounds__(256) void k_fit_merge(long long B, int nc_in, int F
 #pragma unroll
     for (int u = 0; u < kMergeUnroll; ++u) {
       const int c = cb + u < c1 ? cb + u : c1 - 1;  // clamped: a re-read, not used
-      const double *o = in + ((long long)c * B + b) * CS::kLen;
-      v[u][0] = o[CS::cnt];
-      v[u][1] = o[CS::first + i];
-      v[u][2] = o[CS::first + j];
-      v[u][3] = o[CS::mean + i];
-      v[u][4] = o[CS::M + e];
-      v[u][5] = o[CS::npair];
-      v[u][6] = o[CS::dmean + i];
-      v[u][7] = o[CS::dmean + j];
-      v[u][8] = o[CS::dM + e];
-      v[u][9] = o[CS::last + i];
-      v[u][10] = o[CS::last + j];
+      const double *o = in + ((long long)c * B + b) * CS.kLen;
+      v[u][0] = o[CS.cnt];
+      v[u][1] = o[CS.first + i];
+      v[u][2] = o[CS.first + j];
+      v[u][3] = o[CS.mean + i];
+      v[u][4] = o[CS.M + e];
+      v[u][5] = o[CS.npair];
+      v[u][6] = o[CS.dmean + i];
+      v[u][7] = o[CS.dmean + j];
+      v[u][8] = o[CS.dM + e];
+      v[u][9] = o[CS.last + i];
+      v[u][10] = o[CS.last + j];
     }
 #pragma unroll
     for (int u = 0; u < kMergeUnroll; ++u) {
@@ -985,18 +994,18 @@ __global__ __launch_bounds__(256) void k_fit_merge(long long B, int nc_in, int F
       have = true;
     }
   }
-  double *w = out + ((long long)g * B + b) * CS::kLen;
-  w[CS::M + e] = s2;
-  w[CS::dM + e] = d2;
+  double *w = out + ((long long)g * B + b) * CS.kLen;
+  w[CS.M + e] = s2;
+  w[CS.dM + e] = d2;
   if (i == j) {
-    w[CS::mean + i] = si;
-    w[CS::dmean + i] = di;
-    w[CS::first + i] = fi;
-    w[CS::last + i] = li;
+    w[CS.mean + i] = si;
+    w[CS.dmean + i] = di;
+    w[CS.first + i] = fi;
+    w[CS.last + i] = li;
   }
   if (e == 0) {
-    w[CS::cnt] = n;
-    w[CS::npair] = np_;
+    w[CS.cnt] = n;
+    w[CS.npair] = np_;
   }
 }
 
@@ -1143,15 +1152,262 @@ __global__ __launch_bounds__(64) void k_fit_final(long long B, const double *__r
   if (status && L == 0) status[b] = n > 0.0 ? 0 : EKS_STATUS_SINGULAR;
 }
 
+// ---------------------------------------------------------------------------
+// Wide models: n = 10..16 observed coordinates (5-8 cameras; the reference
+// fits any camera count, eks/multiview_pca_smoother.py:684-731).  k_fit_accum
+// keeps both packed scatter sums per lane, 2 n (n + 1) / 2 doubles (272 at
+// n = 16: far past the register file), so here each (trajectory, chunk) is
+// served by a group of kNW = 16 lanes, lane i owning column i: its ensemble,
+// S1_i, D1_i and ROW i of the two scatter sums; the other columns of a frame
+// arrive by shuffles inside the group.  The partial rows have k_fit_accum's
+// layout, so k_fit_merge (N = 0: runtime n) merges them; k_fitw_final does
+// the PCA of the n x n matrix with one 256-thread block (lane (i, j), LDS).
+// ---------------------------------------------------------------------------
+constexpr int kNW = 16;
+
+// one lane per (trajectory, frame): the ensemble of the frame's n columns
+// (runtime E), v_t = max_j var, the shift K (frame 0) and the hand-off planes
+template <typename T, typename YT>
+__global__ __launch_bounds__(256) void k_fitw_worst(const T *__restrict__ obs, FitShape sh,
+                                                    long long sb, long long st, long long se,
+                                                    long long sj, int Ert, int n, int median,
+                                                    double *__restrict__ worst, YevOut yo,
+                                                    FitShift ks) {
+  const long long lane = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (lane >= sh.B * sh.T) return;
+  const long long b = lane / sh.T, t = lane - b * sh.T;
+  const T *p = obs + b * sb + t * st;
+  double v = -1.0;
+  bool nan = false;
+  for (int j = 0; j < n; ++j) {
+    double avg, var;
+    ensemble_reduce_rt<T>(p + j * sj, se, Ert, median != 0, avg, var);
+    nan |= (var != var);
+    v = var > v ? var : v;
+    if (t == 0) ks.K[b * n + j] = avg;
+    if (yo.y) {
+      ((YT *)yo.y)[(t * n + j) * sh.B + b] = (YT)avg;
+      yo.ev[(t * n + j) * sh.B + b] = var;
+    }
+  }
+  worst[lane] = nan ? __builtin_nan("") : v;
+}
+
+template <typename T, typename YT, bool FROM_YEV>
+__global__ __launch_bounds__(256) void k_fitw_accum(const T *__restrict__ obs, FitShape sh,
+                                                    long long sb, long long st, long long se,
+                                                    long long sj, int Ert, int n, int median,
+                                                    const double *__restrict__ thr,
+                                                    const uint64_t *__restrict__ kept,
+                                                    long long W, double *__restrict__ part,
+                                                    YevOut yi, FitShift ks) {
+  const long long gl = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  const long long pc = gl / kNW;  // (chunk, trajectory) pair: c * B + b
+  if (pc >= sh.B * sh.NC) return;  // whole groups (B NC kNW lanes)
+  const int i = (int)(gl % kNW), base = (int)(threadIdx.x & 63) & ~(kNW - 1);
+  const bool own = i < n;
+  const int ic = own ? i : n - 1;  // idle lanes shadow the last column (never stored)
+  const long long b = pc % sh.B, c = pc / sh.B;
+  const long long t0 = c * sh.Lc < sh.T ? c * sh.Lc : sh.T;
+  const long long t1 = t0 + sh.Lc < sh.T ? t0 + sh.Lc : sh.T;
+  const T *pb = obs + b * sb + ic * sj;
+  const double th = thr[b];
+  const uint64_t *krow = FROM_YEV ? kept + b * W : nullptr;
+  const double K = ks.K[b * n + ic];
+  double S2[kNW], D2[kNW];
+#pragma unroll
+  for (int j = 0; j < kNW; ++j) S2[j] = D2[j] = 0.0;
+  double cnt = 0.0, npair = 0.0, S1 = 0.0, D1 = 0.0, first = 0.0, last = 0.0;
+  uint64_t kw = (FROM_YEV && t0 < t1) ? krow[t0 >> 6] : 0ull;
+  for (long long t = t0; t < t1; ++t) {
+    double y;
+    if constexpr (FROM_YEV) {
+      if ((t & 63) == 0) kw = krow[t >> 6];
+      if (!((kw >> (t & 63)) & 1ull)) continue;  // uniform over the group
+      y = (double)((const YT *)yi.y)[(t * n + ic) * sh.B + b];
+    } else {
+      double var;
+      ensemble_reduce_rt<T>(pb + t * st, se, Ert, median != 0, y, var);
+      // v = max over the group's columns, NaN if any is NaN (frame_ensemble)
+      // (a NaN variance made the threshold NaN: nothing is kept either way)
+      double v = var;
+#pragma unroll
+      for (int w = kNW / 2; w >= 1; w >>= 1) {
+        const double o = __shfl_xor(v, w, 64);
+        v = o > v ? o : v;
+      }
+      if (!(v <= th)) continue;  // uniform over the group
+    }
+    if (cnt == 0.0) {
+      first = y;
+    } else {
+      const double d = y - last;
+      D1 += d;
+#pragma unroll
+      for (int j = 0; j < kNW; ++j) D2[j] = fma(d, __shfl(d, base + j, 64), D2[j]);
+      npair += 1.0;
+    }
+    const double z = y - K;
+    last = y;
+    S1 += z;
+#pragma unroll
+    for (int j = 0; j < kNW; ++j) S2[j] = fma(z, __shfl(z, base + j, 64), S2[j]);
+    cnt += 1.0;
+  }
+  const CsRt CS(n);
+  double *o = part + pc * (long long)CS.kLen;
+  if (i == 0) {
+    o[CS.cnt] = cnt;
+    o[CS.npair] = npair;
+  }
+  if (!own) return;
+  o[CS.mean + i] = S1;
+  o[CS.dmean + i] = D1;
+  o[CS.first + i] = first;
+  o[CS.last + i] = last;
+#pragma unroll
+  for (int j = 0; j < kNW; ++j)
+    if (j >= i && j < n) {
+      o[CS.M + CS.tri(i, j)] = S2[j];
+      o[CS.dM + CS.tri(i, j)] = D2[j];
+    }
+}
+
+// k_fit_final's PCA model for n = 10..16 (even): one 256-thread block per
+// trajectory, thread (i, j) = (L / 16, L % 16) owning entry (i, j); the
+// round-robin Jacobi's cross-entry reads go through LDS
+template <int R>
+__global__ __launch_bounds__(256) void k_fitw_final(long long B, const double *__restrict__ part,
+                                                    FitShift ks, int n, double smooth_param,
+                                                    double *__restrict__ params,
+                                                    int32_t *__restrict__ status) {
+  __shared__ double sA[kNW * kNW], sV[kNW * kNW], sM[kNW * kNW], sD[kNW * kNW], sEv[kNW];
+  __shared__ double sRed[2][4];
+  const CsRt CS(n);
+  const long long b = blockIdx.x;
+  const int L = threadIdx.x, i = L / kNW, j = L % kNW;
+  const bool own = i < n && j < n;
+  const double *o = part + b * CS.kLen;
+  const double cnt = o[CS.cnt];
+  double np_ = o[CS.npair];
+  if (np_ < 1.0) np_ = __builtin_nan("");
+  const int ti = own ? (i <= j ? CS.tri(i, j) : CS.tri(j, i)) : 0;
+  const double s1i = own ? o[CS.mean + i] : 0.0, s1j = own ? o[CS.mean + j] : 0.0;
+  const double d1i = own ? o[CS.dmean + i] : 0.0, d1j = own ? o[CS.dmean + j] : 0.0;
+  const double Mij = own ? o[CS.M + ti] - s1i * (s1j / cnt) : 0.0;
+  const double Dij = own ? o[CS.dM + ti] - d1i * (d1j / np_) : 0.0;
+  // packed row [m0 | S0 | A | Q | C (n x R) | offset (n)]
+  const int pS0 = R, pA = R + R * R, pQ = R + 2 * R * R, pC = R + 3 * R * R, pOff = pC + n * R;
+  double *pr = params + b * (long long)(pOff + n);
+  if (L < R) pr[L] = 0.0;
+  if (L < R * R) pr[pA + L] = (L / R == L % R) ? 1.0 : 0.0;
+  if (L < n) pr[pOff + L] = ks.K[b * n + L] + o[CS.mean + L] / cnt;
+  double a = Mij, v = (own && i == j) ? 1.0 : 0.0;
+  const int Nm = n - 1;
+  auto slot_of = [&](int x, int k) { return x == 0 ? 0 : 1 + (x - 1 + Nm - (k % Nm)) % Nm; };
+  auto idx_at = [&](int pos, int k) { return pos == 0 ? 0 : 1 + (pos - 1 + k) % Nm; };
+  for (int sweep = 0; sweep < 60; ++sweep) {
+    double off = (own && i < j) ? a * a : 0.0, dia = (own && i == j) ? a * a : 0.0;
+#pragma unroll
+    for (int w = 32; w >= 1; w >>= 1) {
+      off += __shfl_xor(off, w, 64);
+      dia += __shfl_xor(dia, w, 64);
+    }
+    if ((L & 63) == 0) {
+      sRed[0][L >> 6] = off;
+      sRed[1][L >> 6] = dia;
+    }
+    __syncthreads();
+    off = sRed[0][0] + sRed[0][1] + sRed[0][2] + sRed[0][3];
+    dia = sRed[1][0] + sRed[1][1] + sRed[1][2] + sRed[1][3];
+    __syncthreads();
+    if (off == 0.0 || off <= 1e-34 * dia) break;  // block-uniform
+    for (int k = 0; k < Nm; ++k) {
+      sA[L] = a;
+      sV[L] = v;
+      __syncthreads();
+      auto partner = [&](int x) { return idx_at(Nm - slot_of(x, k), k); };
+      const int li = own ? i : 0, lj = own ? j : 0;
+      const int pi = partner(li), pj = partner(lj);
+      auto rot = [&](int x, int px, double &jxx, double &jpx) {
+        const int p = x < px ? x : px, q = x < px ? px : x;
+        const double apq = sA[p * kNW + q], app = sA[p * kNW + p], aqq = sA[q * kNW + q];
+        double cs = 1.0, sn = 0.0;
+        if (apq != 0.0) {
+          const double theta = (aqq - app) / (2.0 * apq);
+          const double t = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+          cs = 1.0 / sqrt(t * t + 1.0);
+          sn = t * cs;
+        }
+        jxx = cs;
+        jpx = x == p ? -sn : sn;
+      };
+      double ji, jpi_i, jj, jpj_j;
+      rot(li, pi, ji, jpi_i);
+      rot(lj, pj, jj, jpj_j);
+      const double a_ipj = sA[li * kNW + pj], a_pij = sA[pi * kNW + lj];
+      const double a_pipj = sA[pi * kNW + pj], v_ipj = sV[li * kNW + pj];
+      __syncthreads();
+      if (own) {
+        const double r0 = a * jj + a_ipj * jpj_j;
+        const double r1 = a_pij * jj + a_pipj * jpj_j;
+        a = ji * r0 + jpi_i * r1;
+        v = v * jj + v_ipj * jpj_j;
+      }
+    }
+  }
+  sV[L] = v;
+  sM[L] = Mij;
+  sD[L] = Dij;
+  if (own && i == j) sEv[i] = a;
+  __syncthreads();
+  int order[R];
+  unsigned used = 0;
+#pragma unroll
+  for (int k = 0; k < R; ++k) {  // k-th largest eigenvalue (first index on ties)
+    int best = -1;
+    for (int e = 0; e < n; ++e)
+      if (!((used >> e) & 1u) && (best < 0 || sEv[e] > sEv[best])) best = e;
+    order[k] = best;
+    used |= 1u << best;
+  }
+  if (L < R * R) {
+    const int k = L / R, l = L % R;
+    int ok_ = 0, ol = 0;
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      ok_ = u == k ? order[u] : ok_;
+      ol = u == l ? order[u] : ol;
+    }
+    double s0 = 0.0, q = 0.0;
+    for (int x = 0; x < n; ++x)
+      for (int y = 0; y < n; ++y) {
+        const double w = sV[x * kNW + ok_] * sV[y * kNW + ol];
+        s0 = fma(w, sM[x * kNW + y], s0);
+        q = fma(w, sD[x * kNW + y], q);
+      }
+    pr[pS0 + L] = k == l ? s0 / cnt : 0.0;
+    pr[pQ + L] = smooth_param * (q / (np_ - 1.0));
+  }
+  if (own && j < R) {
+    int oj = 0;
+#pragma unroll
+    for (int u = 0; u < R; ++u) oj = u == j ? order[u] : oj;
+    pr[pC + i * R + j] = sV[i * kNW + oj];
+  }
+  if (status && L == 0) status[b] = cnt > 0.0 ? 0 : EKS_STATUS_SINGULAR;
+}
+
 // chunks per trajectory (k_fit_worst's and k_fit_accum's lanes): enough
-// lanes to fill the chip (~256k), chunks of >= kTile frames, a multiple of
-// kTile frames each
-void fit_chunks(long long B, long long T, int &nc, long long &lc) {
-  long long n = (262144 + B - 1) / (B > 0 ? B : 1);
+// lanes to fill the chip (~256k; the wide fit's groups of kNW lanes count
+// kNW each), chunks of >= kTile frames, a multiple of kTile frames each
+void fit_chunks(long long B, long long T, int &nc, long long &lc, int n = 0) {
+  const long long target = n > kMaxObs ? 262144 / kNW : 262144;
+  long long nn = (target + B - 1) / (B > 0 ? B : 1);
   const long long cap = T / kTile > 1 ? T / kTile : 1;
-  if (n > cap) n = cap;
-  if (n < 1) n = 1;
-  lc = (T + n - 1) / n;
+  if (nn > cap) nn = cap;
+  if (nn < 1) nn = 1;
+  lc = (T + nn - 1) / nn;
   lc = (lc + kTile - 1) / kTile * kTile;
   nc = (int)((T + lc - 1) / lc);
 }
@@ -1159,8 +1415,9 @@ void fit_chunks(long long B, long long T, int &nc, long long &lc) {
 constexpr int kMergeFan = 16;
 
 // few long trajectories: k_fit_accum merges each wave's 64 chunks itself
-bool fit_wave_merge(int nc) { return nc >= 64; }
-int fit_partials(int nc) { return fit_wave_merge(nc) ? (nc + 63) / 64 : nc; }
+bool fit_wave_merge(int nc, int n = 0) { return n <= kMaxObs && nc >= 64; }
+int fit_partials(int nc, int n = 0) { return fit_wave_merge(nc, n) ? (nc + 63) / 64 : nc; }
+constexpr int kMaxObsFit = kNW;  // n of eks_fit (even; n > kMaxObs: the wide kernels)
 
 }  // namespace
 
@@ -1169,12 +1426,12 @@ int fit_partials(int nc) { return fit_wave_merge(nc) ? (nc + 63) / 64 : nc; }
 using namespace eks;
 
 extern "C" size_t eks_fit_workspace_bytes(int64_t B, int64_t T, int n) {
-  if (B <= 0 || T <= 0 || n < 1 || n > kMaxObs) return 0;
+  if (B <= 0 || T <= 0 || n < 1 || n > kMaxObsFit) return 0;
   int nc;
   long long lc;
-  fit_chunks(B, T, nc, lc);
+  fit_chunks(B, T, nc, lc, n);
   const long long len = 2 + 4LL * n + (long long)n * (n + 1);
-  const long long np = fit_partials(nc);
+  const long long np = fit_partials(nc, n);
   const long long nc2 = (np + kMergeFan - 1) / kMergeFan;
   const long long W = (T + 63) / 64;  // frame-mask words per trajectory
   // worst plane, thresholds, chunk partials, kept-frame mask, shifts K
@@ -1227,12 +1484,12 @@ extern "C" int eks_fit(const void *obs, int obs_dtype, int64_t B, int64_t T, int
                    eks_fit_workspace_bytes(B, T, n));
   hipStream_t s = (hipStream_t)stream;
   FitShape sh{B, T, 0, 0};
-  fit_chunks(B, T, sh.NC, sh.Lc);
+  fit_chunks(B, T, sh.NC, sh.Lc, n);
   const long long len = 2 + 4LL * n + (long long)n * (n + 1);
   double *worst = (double *)workspace;
   double *thr = worst + B * T;
-  const int npart = fit_partials(sh.NC);
-  const bool wave_merge = fit_wave_merge(sh.NC);
+  const int npart = fit_partials(sh.NC, n);
+  const bool wave_merge = fit_wave_merge(sh.NC, n);
   double *partA = thr + B;
   double *partB = partA + B * (long long)npart * len;
   const long long W = (T + 63) / 64;
@@ -1261,10 +1518,92 @@ extern "C" int eks_fit(const void *obs, int obs_dtype, int64_t B, int64_t T, int
     yo.y = yev;
     yo.ev = (double *)((char *)yev + yev_ev_offset(B, T, n, y32 ? 4 : 8));
   }
+  // the order statistics, the threshold and (with the hand-off planes
+  // written) the kept-frame mask k_fit_accum reads instead of the ev plane
+  auto select = [&]() -> int {
+    prof_mark(s, "k_fit_select");
+    if (split_sel) {
+      // few long rows: one block per (row, segment) in four launches
+      if (hipMemsetAsync(ghist, 0, (size_t)B * kBins * 4 + (size_t)B * sizeof(SelRow), s) !=
+          hipSuccess)
+        return set_err(EKS_ERR_HIP, "eks_fit: hipMemsetAsync failed");
+      const unsigned gs = (unsigned)(B * G);
+      prof_mark(s, "k_sel_hist");
+      hipLaunchKernelGGL(k_sel_hist, dim3(gs), dim3(256), 0, s, worst, T, G, ghist, rows);
+      prof_mark(s, "k_sel_bin");
+      hipLaunchKernelGGL(k_sel_bin, dim3((unsigned)B), dim3(256), 0, s, ghist, lo, rows);
+      prof_mark(s, "k_sel_cand");
+      hipLaunchKernelGGL(k_sel_cand, dim3(gs), dim3(256), 0, s, worst, T, G, rows, ckey, cidx,
+                         yev ? kept : nullptr, W);
+      prof_mark(s, "k_sel_final");
+      hipLaunchKernelGGL(k_sel_final<1024>, dim3((unsigned)B), dim3(1024), 0, s, worst, T,
+                         hi - lo, g, rows, ckey, cidx, thr, yev ? kept : nullptr, W);
+    } else if (T >= 65536) {
+      hipLaunchKernelGGL(k_fit_select<1024>, dim3((unsigned)B), dim3(1024), 0, s, worst, T,
+                         lo, hi, g, thr, yev ? kept : nullptr, W);
+    } else {
+      hipLaunchKernelGGL(k_fit_select<256>, dim3((unsigned)B), dim3(256), 0, s, worst, T, lo,
+                         hi, g, thr, yev ? kept : nullptr, W);
+    }
+    return check_launch("k_fit_select");
+  };
+  // merge the chunk partials in order, kMergeFan at a time, ping-pong
+  auto merge = [&](auto Nc, int npart_) -> double * {
+    constexpr int NN = decltype(Nc)::value;
+    double *src = partA, *dst = partB;
+    int nc = npart_;
+    const long long tri = (long long)n * (n + 1) / 2;
+    while (nc > 1) {
+      const int nout = (nc + kMergeFan - 1) / kMergeFan;
+      prof_mark(s, "k_fit_merge");
+      hipLaunchKernelGGL((k_fit_merge<NN>), dim3(grid_for(B * (long long)nout * tri, 256)),
+                         dim3(256), 0, s, B, nc, kMergeFan, src, dst, n);
+      if (check_launch("k_fit_merge")) return nullptr;
+      double *t = src;
+      src = dst;
+      dst = t;
+      nc = nout;
+    }
+    return src;
+  };
   // keypoint observations come in (x, y) pairs: n = 2 (single view) or 2V
   // (V cameras); the odd n are not compiled (they doubled this unit's code)
-  if (n % 2 != 0 || n > kMaxObs)
-    return set_err(EKS_ERR_UNSUPPORTED, "eks_fit: n=%d not supported (2, 4, 6, 8)", n);
+  if (n % 2 != 0 || n > kMaxObsFit)
+    return set_err(EKS_ERR_UNSUPPORTED, "eks_fit: n=%d not supported (even, <= %d)", n, kMaxObsFit);
+  if (n > kMaxObs) {  // 5-8 cameras: the wide kernels (runtime n, runtime E)
+    if (kind != EKS_FIT_MULTICAM || r != 3)
+      return set_err(EKS_ERR_UNSUPPORTED, "eks_fit: n=%d needs the PCA model with r = 3", n);
+    auto wide = [&](auto tag, auto ytag) -> int {
+      using Tp = decltype(tag);
+      using YT = decltype(ytag);
+      prof_call_begin();
+      prof_mark(s, "k_fitw_worst");
+      hipLaunchKernelGGL((k_fitw_worst<Tp, YT>), dim3(grid_for(B * T, 256)), dim3(256), 0, s,
+                         (const Tp *)obs, sh, sb, st, se, sj, E, n, median, worst, yo, ks);
+      int rc = check_launch("k_fitw_worst");
+      if (rc || (rc = select())) return rc;
+      prof_mark(s, "k_fitw_accum");
+      const unsigned ga = grid_for(B * (long long)sh.NC * kNW, 256);
+      if (yev)
+        hipLaunchKernelGGL((k_fitw_accum<Tp, YT, true>), dim3(ga), dim3(256), 0, s,
+                           (const Tp *)obs, sh, sb, st, se, sj, E, n, median, thr, kept, W, partA,
+                           yo, ks);
+      else
+        hipLaunchKernelGGL((k_fitw_accum<Tp, YT, false>), dim3(ga), dim3(256), 0, s,
+                           (const Tp *)obs, sh, sb, st, se, sj, E, n, median, thr, kept, W, partA,
+                           yo, ks);
+      if ((rc = check_launch("k_fitw_accum"))) return rc;
+      double *src = merge(ic<0>{}, npart);
+      if (!src) return EKS_ERR_HIP;
+      prof_mark(s, "k_fitw_final");
+      hipLaunchKernelGGL((k_fitw_final<3>), dim3((unsigned)B), dim3(256), 0, s, B, src, ks, n,
+                         smooth_param, params, status);
+      prof_call_end(s);
+      return check_launch("k_fitw_final");
+    };
+    if (y32) return wide(float{}, float{});
+    return obs_dtype == EKS_F32 ? wide(float{}, double{}) : wide(double{}, double{});
+  }
   auto dispatch_even = [&](auto &&f) -> int {
     switch (n) {
       case 2: return f(ic<2>{});
@@ -1286,33 +1625,7 @@ extern "C" int eks_fit(const void *obs, int obs_dtype, int64_t B, int64_t T, int
                            (const Tp *)obs, sh, sb, st, se, sj, E, median, worst, yo, ks);
         int rc = check_launch("k_fit_worst");
         if (rc) return rc;
-        prof_mark(s, "k_fit_select");
-        // with the hand-off planes written, the selection also writes the
-        // kept-frame mask k_fit_accum reads instead of the ev plane
-        if (split_sel) {
-          // few long rows: one block per (row, segment) in four launches
-          if (hipMemsetAsync(ghist, 0, (size_t)B * kBins * 4 + (size_t)B * sizeof(SelRow), s) !=
-              hipSuccess)
-            return set_err(EKS_ERR_HIP, "eks_fit: hipMemsetAsync failed");
-          const unsigned gs = (unsigned)(B * G);
-          prof_mark(s, "k_sel_hist");
-          hipLaunchKernelGGL(k_sel_hist, dim3(gs), dim3(256), 0, s, worst, T, G, ghist, rows);
-          prof_mark(s, "k_sel_bin");
-          hipLaunchKernelGGL(k_sel_bin, dim3((unsigned)B), dim3(256), 0, s, ghist, lo, rows);
-          prof_mark(s, "k_sel_cand");
-          hipLaunchKernelGGL(k_sel_cand, dim3(gs), dim3(256), 0, s, worst, T, G, rows, ckey, cidx,
-                             yev ? kept : nullptr, W);
-          prof_mark(s, "k_sel_final");
-          hipLaunchKernelGGL(k_sel_final<1024>, dim3((unsigned)B), dim3(1024), 0, s, worst, T,
-                             hi - lo, g, rows, ckey, cidx, thr, yev ? kept : nullptr, W);
-        } else if (T >= 65536) {
-          hipLaunchKernelGGL(k_fit_select<1024>, dim3((unsigned)B), dim3(1024), 0, s, worst, T,
-                             lo, hi, g, thr, yev ? kept : nullptr, W);
-        } else {
-          hipLaunchKernelGGL(k_fit_select<256>, dim3((unsigned)B), dim3(256), 0, s, worst, T, lo,
-                             hi, g, thr, yev ? kept : nullptr, W);
-        }
-        if ((rc = check_launch("k_fit_select"))) return rc;
+        if ((rc = select())) return rc;
         prof_mark(s, "k_fit_accum");
         // with the hand-off planes written, the second pass reads the y plane
         // and the frame mask (8 B per frame for n = 2 with float32 y) instead
@@ -1332,21 +1645,8 @@ extern "C" int eks_fit(const void *obs, int obs_dtype, int64_t B, int64_t T, int
           else accum(ic<0>{}, ic<0>{});
         }
         if ((rc = check_launch("k_fit_accum"))) return rc;
-        // merge the chunk partials in order, kMergeFan at a time, ping-pong
-        double *src = partA, *dst = partB;
-        int nc = npart;
-        while (nc > 1) {
-          const int nout = (nc + kMergeFan - 1) / kMergeFan;
-          const long long threads = B * (long long)nout * ChunkStats<NN>::kTri;
-          prof_mark(s, "k_fit_merge");
-          hipLaunchKernelGGL((k_fit_merge<NN>), dim3(grid_for(threads, 256)), dim3(256), 0, s, B,
-                             nc, kMergeFan, src, dst);
-          if ((rc = check_launch("k_fit_merge"))) return rc;
-          double *t = src;
-          src = dst;
-          dst = t;
-          nc = nout;
-        }
+        double *src = merge(Nc, npart);
+        if (!src) return EKS_ERR_HIP;
         prof_mark(s, "k_fit_final");
         rc = dispatch_r(r, [&](auto Rc) {
           constexpr int RR = decltype(Rc)::value;

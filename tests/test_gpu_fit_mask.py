@@ -159,7 +159,7 @@ def test_mask_nan_row(torch):
     _vs_host(st[ok], p[ok], 25.0)
 
 
-@pytest.mark.parametrize("V", [2, 4])
+@pytest.mark.parametrize("V", [2, 4, 5, 8])
 def test_mask_multicam(torch, V):
     from eks_amd import synthetic
     rng = np.random.default_rng(V)

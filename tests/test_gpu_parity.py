@@ -675,8 +675,11 @@ def test_fit_singleview_one_kept_frame(torch):
         np.testing.assert_array_equal(ref["offset"], got["offset"])
 
 
-@pytest.mark.parametrize("V,T", [(2, 2000), (4, 1500), (3, 700)])
+@pytest.mark.parametrize("V,T", [(2, 2000), (4, 1500), (3, 700), (5, 3000), (6, 1500),
+                                 (8, 700)])
 def test_fit_multicam_vs_host(torch, V, T):
+    """V >= 5 (n = 10..16) runs the wide kernels (k_fitw_*: 16-lane groups,
+    one 256-thread block's Jacobi)."""
     from eks_amd import batch, fit, synthetic
     from eks_amd.core import ensemble_array
     rng = np.random.default_rng(V * T)
