@@ -57,6 +57,8 @@ def parse():
                     help="BASELINE.json configuration (1-based index)")
     ap.add_argument("--videos", type=int, default=1024, help="config 4: videos in the batch")
     ap.add_argument("--keypoints", type=int, default=17)
+    ap.add_argument("--cameras", type=int, default=4,
+                    help="config 3: cameras V (n = 2V; V > 4 runs the runtime-n kernels)")
     ap.add_argument("--members", type=int, default=5)
     ap.add_argument("--frames", type=int, default=None,
                     help="frames per video (default: 10k / 100k / 50k / 1M for configs 4/2/3/5)")
@@ -314,10 +316,10 @@ def workload_singleview(torch, a, dev, rank, world, config):
 
 
 def workload_multiview(torch, a, dev, rank, world):
-    """config 3: V = 4 cameras x 17 keypoints x 50k frames, PCA multiview."""
+    """config 3: V cameras (4 by default) x 17 keypoints x 50k frames, PCA multiview."""
     import numpy as np
     from eks_amd import _lib, batch, fit, synthetic
-    K, E, T, V = a.keypoints, a.members, a.frames, 4
+    K, E, T, V = a.keypoints, a.members, a.frames, a.cameras
     rng = np.random.default_rng(a.seed)
     st = synthetic.multiview_obs(rng, V, E, T, K=K)                   # (E, T, K, 8) f32
     n = 2 * V
@@ -353,12 +355,13 @@ def workload_multiview(torch, a, dev, rank, world):
                     what=f"{{n}} keypoints x {T} frames x {V} cameras of this workload")
 
     desc = (f"config 3: multiview PCA smoother, {V} cameras x {K} keypoints x {E} members x "
-            f"{T} frames (r=3 latent, n=8), float32 members, float64 recursions/outputs")
+            f"{T} frames (r=3 latent, n={n}), float32 members, float64 recursions/outputs")
     return dict(step=step, fit_step=fit_step, e2e_smooth=e2e_smooth, status=status,
                 units=K * T, bytes_per_unit=E * n * 4 + n * 8, cpu_plan=cpu_plan, desc=desc,
                 cfg=dict(cameras=V, keypoints=K, members=E, frames=T,
                          smooth_param=a.smooth_param, quantile_keep=a.quantile_keep),
-                shape=(K, T, n, 3, E), key=f"config3-multiview-k{K}-e{E}-t{T}")
+                shape=(K, T, n, 3, E),
+                key=f"config3-multiview-k{K}-e{E}-t{T}" + (f"-v{V}" if V != 4 else ""))
 
 
 def workload_pupil(torch, a, dev, rank, world):

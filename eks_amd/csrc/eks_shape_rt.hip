@@ -79,15 +79,24 @@ __global__ __launch_bounds__(64) void k_smooth_seq_rt(SmoothArgs a) {
   const double *C = pp + R + 3 * R * R;  // n x R, row-major
   const double *off = C + (long long)n * R;
   double *ws = (double *)a.ws;
-  const T *ob = (const T *)a.obs + b * a.sb;
+  constexpr bool kYev = is_yev<T>::value;  // the caller's y / ev planes (EKS_YEV32 / 64)
+  using YT = typename yev_y<T>::type;
+  const YT *ob = (const YT *)a.obs + (kYev ? 0 : b * a.sb);
+  const double *evp = kYev ? (const double *)((const char *)a.obs +
+                                              yev_ev_offset(B, TT, n, sizeof(YT)))
+                           : nullptr;
   bool ok = true;
   NllAcc acc;
   for (long long t = 0; t < TT; ++t) {
     if (t > 0) kf_predict<R, kAGen>(m, P, A, Q);
-    const T *pt = ob + t * a.st;
     for (int j = 0; j < n; ++j) {
       double avg, var;
-      ensemble_reduce_rt<T>(pt + j * a.sj, a.se, a.E, median, avg, var);
+      if constexpr (kYev) {
+        avg = (double)ob[(t * n + j) * B + b];
+        var = evp[(t * n + j) * B + b];
+      } else {
+        ensemble_reduce_rt<YT>(ob + t * a.st + j * a.sj, a.se, a.E, median, avg, var);
+      }
       kf_update_row_rt<R>(m, P, C + j * R, avg - off[j], var, acc, ok);
     }
     acc.renorm();
@@ -163,8 +172,10 @@ __global__ __launch_bounds__(kBlock) void k_rt_c1(SmoothArgs a, ChunkPlan p) {
   load_mat<R, R>(pp + L::A, A);
   load_mat<R, R>(pp + L::Q, Q);
   const double *C = pp + L::C, *off = C + (long long)n * R;
+  constexpr bool kYev = is_yev<T>::value;  // the caller's y / ev planes (EKS_YEV32 / 64)
+  using YT = typename yev_y<T>::type;
   double *ybuf = (double *)(a.ws + p.y_off), *evbuf = (double *)(a.ws + p.ev_off);
-  const T *ob = (const T *)a.obs + (long long)b * a.sb;
+  const YT *ob = kYev ? nullptr : (const YT *)a.obs + (long long)b * a.sb;
   const long long s = c * p.L, e = min(TT, s + p.L);
   const bool first = c == 0;
   bool ok = true;
@@ -182,12 +193,16 @@ __global__ __launch_bounds__(kBlock) void k_rt_c1(SmoothArgs a, ChunkPlan p) {
     } else {
       elem_predict<R, kAGen>(El, A, Q);
     }
-    const T *pt = ob + t * a.st;
     for (int j = 0; j < n; ++j) {
       double avg, var, cr[R];
-      ensemble_reduce_rt<T>(pt + j * a.sj, a.se, a.E, median, avg, var);
-      pl(ybuf, t * n + j, B, b) = avg;
-      pl(evbuf, t * n + j, B, b) = var;
+      if constexpr (kYev) {
+        avg = (double)pl((const YT *)p.ysrc, t * n + j, B, b);
+        var = pl((const double *)p.evsrc, t * n + j, B, b);
+      } else {
+        ensemble_reduce_rt<YT>(ob + t * a.st + j * a.sj, a.se, a.E, median, avg, var);
+        pl(ybuf, t * n + j, B, b) = avg;
+        pl(evbuf, t * n + j, B, b) = var;
+      }
       load_row<R>(C + j * R, cr);
       if (first)
         kf_update_row_rt<R>(m, P, cr, avg - off[j], var, acc, ok);
@@ -211,7 +226,7 @@ __global__ __launch_bounds__(kBlock) void k_rt_c1(SmoothArgs a, ChunkPlan p) {
   if (!ok) flag(a.status, b, first ? EKS_STATUS_SINGULAR : EKS_STATUS_SCAN);
 }
 
-template <int R>
+template <int R, typename YT>
 __global__ __launch_bounds__(kBlock) void k_rt_c3(SmoothArgs a, ChunkPlan p) {
   Lane<false> ln;
   if (!ln.init(a.B, p.NC)) return;
@@ -226,7 +241,8 @@ __global__ __launch_bounds__(kBlock) void k_rt_c3(SmoothArgs a, ChunkPlan p) {
   load_mat<R, R>(pp + L::A, A);
   load_mat<R, R>(pp + L::Q, Q);
   const double *C = pp + L::C, *off = C + (long long)n * R;
-  const double *ybuf = (const double *)(a.ws + p.y_off), *evbuf = (const double *)(a.ws + p.ev_off);
+  const YT *ybuf = (const YT *)p.ysrc;
+  const double *evbuf = (const double *)p.evsrc;
   double *jdp = (double *)(a.ws + p.jd_off);
   double m[R], P[R][R], G[R][R], g[R];
   load_state_pl<R>((const double *)(a.ws + p.cstart_off), c * KS, B, b, m, P);
@@ -244,7 +260,7 @@ __global__ __launch_bounds__(kBlock) void k_rt_c3(SmoothArgs a, ChunkPlan p) {
     for (int j = 0; j < n; ++j) {
       double cr[R];
       load_row<R>(C + j * R, cr);
-      kf_update_row_rt<R>(m, P, cr, pl(ybuf, t * n + j, B, b) - off[j],
+      kf_update_row_rt<R>(m, P, cr, (double)pl(ybuf, t * n + j, B, b) - off[j],
                           pl(evbuf, t * n + j, B, b), acc, ok);
     }
     acc.renorm();
@@ -349,6 +365,14 @@ int launch_rt_chunked(const SmoothArgs &a) {
   p.smooth = a.out != nullptr;
   p.yB = a.B;
   p.jd = p.smooth ? 1 : 0;
+  using YT = typename yev_y<T>::type;
+  if constexpr (is_yev<T>::value) {
+    p.ysrc = (const char *)a.obs;
+    p.evsrc = p.ysrc + yev_ev_offset(a.B, a.T, a.n, sizeof(YT));
+  } else {
+    p.ysrc = a.ws + p.y_off;
+    p.evsrc = a.ws + p.ev_off;
+  }
   const unsigned gch = grid_for(p.NC * a.B, kBlock), g64 = grid_for(a.B, 64);
   const bool wave_scan = p.NC > wave_scan_chunks();
   int rc;
@@ -364,7 +388,7 @@ int launch_rt_chunked(const SmoothArgs &a) {
                        a, p);
   if ((rc = check_launch("k_c2_fscan"))) return rc;
   prof_mark(a.stream, "k_rt_c3");
-  hipLaunchKernelGGL((k_rt_c3<R>), dim3(gch), dim3(kBlock), 0, a.stream, a, p);
+  hipLaunchKernelGGL((k_rt_c3<R, YT>), dim3(gch), dim3(kBlock), 0, a.stream, a, p);
   if ((rc = check_launch("k_rt_c3"))) return rc;
   if (!p.smooth) {
     prof_mark(a.stream, "k_c4_nll");
@@ -386,11 +410,9 @@ int launch_rt_chunked(const SmoothArgs &a) {
 }
 
 int launch_rt(const SmoothArgs &a) {
-  if (a.dtype != EKS_F32 && a.dtype != EKS_F64)
-    return set_err(EKS_ERR_UNSUPPORTED,
-                   "eks_smooth: (r=%d, n=%d) runs the runtime-n kernel, which reads member "
-                   "predictions (f32 / f64), not y / ev planes", a.r, a.n);
-  const bool chunked = rt_chunked(a.B, a.T, a.r);
+  // algo 1 asks for the sequential form (batch.smooth's re-run after a
+  // time-parallel breakdown)
+  const bool chunked = a.algo != 1 && rt_chunked(a.B, a.T, a.r);
   auto go = [&](auto rtag, auto ttag) -> int {
     constexpr int R = decltype(rtag)::value;
     using T = decltype(ttag);
@@ -402,10 +424,17 @@ int launch_rt(const SmoothArgs &a) {
     prof_call_end(a.stream);
     return check_launch("k_smooth_seq_rt");
   };
-  const bool f32 = a.dtype == EKS_F32;
+  auto by_type = [&](auto rtag) -> int {
+    switch (a.dtype) {
+      case EKS_F32: return go(rtag, float{});
+      case EKS_F64: return go(rtag, double{});
+      case EKS_YEV32: return go(rtag, YevIn<float>{});
+      default: return go(rtag, YevIn<double>{});
+    }
+  };
   switch (a.r) {
-    case 2: return f32 ? go(ic<2>{}, float{}) : go(ic<2>{}, double{});
-    case 3: return f32 ? go(ic<3>{}, float{}) : go(ic<3>{}, double{});
+    case 2: return by_type(ic<2>{});
+    case 3: return by_type(ic<3>{});
     default:
       return set_err(EKS_ERR_UNSUPPORTED, "eks_smooth: latent r=%d not compiled in (2, 3)", a.r);
   }

@@ -104,7 +104,8 @@ static int smooth_call(const void *obs, int obs_dtype, int64_t B, int64_t T, int
   if ((model_flags & EKS_MODEL_PUPIL) && (r != 3 || n != 8))
     return set_err(EKS_ERR_ARG, "eks_smooth: EKS_MODEL_PUPIL needs r = 3, n = 8");
   if (B == 0) return EKS_OK;
-  int al = rt ? 4 : phase ? 2 : pick_algo(B, T, n, r, E, algo);
+  // (the runtime-n kernels: algo 1 picks their sequential form)
+  int al = rt ? (algo == 1 ? 1 : 4) : phase ? 2 : pick_algo(B, T, n, r, E, algo);
   const size_t need = phase ? make_plan(B, T, r, n, chunk_len(B, T, r)).total
                             : eks_smooth_workspace_bytes(B, T, n, r, E, al);
   if (!workspace || workspace_bytes < need)

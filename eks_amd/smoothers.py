@@ -28,12 +28,11 @@ def _run_fused(stack: np.ndarray, model: dict, mode: str = "median", want_ms=Fal
     """stack (E, T, n) float64 host array + model -> out (T, n), ms, nll.
     With ``yev`` (core.ensemble_handoff's planes of the same stack) the
     smoother reads the planes instead of uploading and reducing the members
-    again -- except on the runtime-n kernel (algo 4: shapes without compiled
-    kernels), which reads member predictions only."""
+    again (every algorithm, the runtime-n kernels included)."""
     torch = _lib.require_gpu()
     E, T, n = stack.shape
     r = len(model["m0"])
-    if yev is not None and _lib.load().eks_smooth_algo(1, T, n, r, E, 0) != 4:
+    if yev is not None:
         obs = yev
     else:
         obs = torch.from_numpy(np.ascontiguousarray(stack, dtype=np.float64)).to("cuda")

@@ -145,3 +145,22 @@ def test_runtime_n_time_parallel_equals_sequential(torch, rt_form, r, n, B, T):
     ms, _, _ = O.smooth_backward(p["y"], mf, Vf, S, p["A"])
     ref = ms @ p["C"].T + p["means"]
     assert np.abs(b_["out"][0].cpu().numpy() - ref).max() < 1e-5
+
+
+@pytest.mark.parametrize("V,E,dtype", [(5, 5, np.float32), (6, 4, np.float64), (8, 3, np.float32)])
+def test_wide_fit_handoff_then_time_parallel_smooth(torch, V, E, dtype):
+    """5-8 cameras end to end on the device: eks_fit (wide kernels) writes the
+    y / ev hand-off planes, and the time-parallel runtime-n smoother reading
+    them equals the same smoother reading the members, bit for bit (the same
+    runtime-E ensemble either way)."""
+    from eks_amd import batch, synthetic
+    rng = np.random.default_rng(V * 10 + E)
+    K, T, n = 3, 4000, 2 * V
+    st = synthetic.multiview_obs(rng, V, E, T, K=K).astype(dtype)      # (E, T, K, n)
+    obs = torch.from_numpy(np.ascontiguousarray(st.transpose(2, 1, 0, 3))).cuda()  # (K, T, E, n)
+    params, _, yev = batch.fit(obs, kind="multicam", n=n, r=3, smooth_param=0.01,
+                               quantile_keep=25, keep_yev=True)
+    a = batch.smooth(obs, params, n=n, r=3, want_nll=True, check=True)
+    b = batch.smooth(yev, params, n=n, r=3, want_nll=True, check=True)
+    assert torch.equal(a["out"], b["out"])
+    assert torch.equal(a["nll"], b["nll"])
