@@ -244,14 +244,22 @@ def multi_cam_batch(stacks, smooth_param, quantile_keep_pca, version: str = "sta
 
     stacks (K, E, T, 2V) camera-major (x, y) columns per keypoint.  The
     per-keypoint model fit is ensemble_kalman_smoother_multi_cam's
-    (eks/multiview_pca_smoother.py:684-731); version "standard" runs the
-    fused RTS smoother (eks_smooth), "opti" the Newton filter
-    (eks_newton_filter, :777-933).  Returns out (K, T, 2V) float64 numpy."""
+    (eks/multiview_pca_smoother.py:684-731); version "standard" fits every
+    keypoint's model on the device (eks_fit, 1-8 cameras) and runs the fused
+    RTS smoother (eks_smooth) on the fit's ensemble hand-off planes, "opti"
+    fits on the host and runs the Newton filter (eks_newton_filter,
+    :777-933).  Returns out (K, T, 2V) float64 numpy."""
     torch = _lib.require_gpu()
     stacks = np.asarray(stacks, dtype=np.float64)
     K, E, T, n = stacks.shape
     if n < 4:
         raise ValueError("multi-camera smoothing needs at least two cameras")
+    if version != "opti" and n % 2 == 0 and n <= 16:
+        obs = torch.from_numpy(np.ascontiguousarray(stacks)).to("cuda").permute(0, 2, 1, 3)
+        params, _, yev = batch.fit(obs, kind="multicam", n=n, r=3, smooth_param=smooth_param,
+                                   quantile_keep=quantile_keep_pca, keep_yev=True)
+        res = batch.smooth(yev, params, n=n, r=3, flags=_lib.EKS_MODEL_A_IDENTITY, check=True)
+        return res["out"].cpu().numpy()
     d, preds_d, ev_d = ensemble_stacks(stacks)
     preds, ev = preds_d.cpu().numpy(), ev_d.cpu().numpy()
     models = [fit.multicam_model(preds[k], ev[k], smooth_param, quantile_keep_pca)
