@@ -1165,32 +1165,63 @@ __global__ __launch_bounds__(64) void k_fit_final(long long B, const double *__r
 // ---------------------------------------------------------------------------
 constexpr int kNW = 16;
 
-// one lane per (trajectory, frame): the ensemble of the frame's n columns
-// (runtime E), v_t = max_j var, the shift K (frame 0) and the hand-off planes
+// k_fit_worst's lanes and tiles (trajectory-fastest lanes over chunks of
+// frames: the hand-off planes' rows, B values each, are written by
+// consecutive lanes; the worst rows leave through an LDS tile) with the
+// frame's n columns reduced in a runtime loop (runtime E)
 template <typename T, typename YT>
 __global__ __launch_bounds__(256) void k_fitw_worst(const T *__restrict__ obs, FitShape sh,
                                                     long long sb, long long st, long long se,
                                                     long long sj, int Ert, int n, int median,
                                                     double *__restrict__ worst, YevOut yo,
                                                     FitShift ks) {
+  __shared__ double tile[256][kTile + 1];
+  __shared__ long long base[256];
   const long long lane = blockIdx.x * (long long)blockDim.x + threadIdx.x;
-  if (lane >= sh.B * sh.T) return;
-  const long long b = lane / sh.T, t = lane - b * sh.T;
-  const T *p = obs + b * sb + t * st;
-  double v = -1.0;
-  bool nan = false;
-  for (int j = 0; j < n; ++j) {
-    double avg, var;
-    ensemble_reduce_rt<T>(p + j * sj, se, Ert, median != 0, avg, var);
-    nan |= (var != var);
-    v = var > v ? var : v;
-    if (t == 0) ks.K[b * n + j] = avg;
-    if (yo.y) {
-      ((YT *)yo.y)[(t * n + j) * sh.B + b] = (YT)avg;
-      yo.ev[(t * n + j) * sh.B + b] = var;
-    }
+  const bool active = lane < sh.B * sh.NC;
+  long long b = 0, t0 = 0, t1 = 0;
+  if (active) {
+    b = lane % sh.B;
+    t0 = (lane / sh.B) * sh.Lc;
+    t1 = t0 + sh.Lc < sh.T ? t0 + sh.Lc : sh.T;
   }
-  worst[lane] = nan ? __builtin_nan("") : v;
+  const T *pb = obs + b * sb;
+  auto frame = [&](long long t) {  // v_t; K and the planes as side effects
+    double v = -1.0;
+    bool nan = false;
+    for (int j = 0; j < n; ++j) {
+      double avg, var;
+      ensemble_reduce_rt<T>(pb + t * st + j * sj, se, Ert, median != 0, avg, var);
+      nan |= (var != var);
+      v = var > v ? var : v;
+      if (t == 0) ks.K[b * n + j] = avg;
+      if (yo.y) {
+        ((YT *)yo.y)[(t * n + j) * sh.B + b] = (YT)avg;
+        yo.ev[(t * n + j) * sh.B + b] = var;
+      }
+    }
+    return nan ? __builtin_nan("") : v;
+  };
+  const long long ntiles = sh.Lc / kTile;  // Lc is a multiple of kTile
+  for (long long kt = 0; kt < ntiles; ++kt) {
+    const long long t = t0 + kt * kTile;
+    if (active && t + kTile <= t1) {
+      for (int k = 0; k < kTile; ++k) tile[threadIdx.x][k] = frame(t + k);
+      base[threadIdx.x] = b * sh.T + t;
+    } else {
+      base[threadIdx.x] = -1;
+      if (active)
+        for (long long u = t; u < t1; ++u) worst[b * sh.T + u] = frame(u);  // ragged end
+    }
+    __syncthreads();
+#pragma unroll
+    for (int p = 0; p < 256 / 16; ++p) {
+      const int r = p * 16 + (threadIdx.x >> 4), k = threadIdx.x & 15;
+      const long long o = base[r];
+      if (o >= 0) worst[o + k] = tile[r][k];
+    }
+    __syncthreads();
+  }
 }
 
 template <typename T, typename YT, bool FROM_YEV>
@@ -1578,8 +1609,12 @@ extern "C" int eks_fit(const void *obs, int obs_dtype, int64_t B, int64_t T, int
       using YT = decltype(ytag);
       prof_call_begin();
       prof_mark(s, "k_fitw_worst");
-      hipLaunchKernelGGL((k_fitw_worst<Tp, YT>), dim3(grid_for(B * T, 256)), dim3(256), 0, s,
-                         (const Tp *)obs, sh, sb, st, se, sj, E, n, median, worst, yo, ks);
+      int ncw;
+      long long lcw;
+      fit_chunks(B, T, ncw, lcw);  // k_fit_worst's lanes (one per (trajectory, chunk))
+      const FitShape shw{B, T, ncw, lcw};
+      hipLaunchKernelGGL((k_fitw_worst<Tp, YT>), dim3(grid_for(B * (long long)ncw, 256)), dim3(256), 0, s,
+                         (const Tp *)obs, shw, sb, st, se, sj, E, n, median, worst, yo, ks);
       int rc = check_launch("k_fitw_worst");
       if (rc || (rc = select())) return rc;
       prof_mark(s, "k_fitw_accum");

@@ -365,7 +365,8 @@ int launch_rt_chunked(const SmoothArgs &a) {
   p.smooth = a.out != nullptr;
   p.yB = a.B;
   p.jd = p.smooth ? 1 : 0;
-  using YT = typename yev_y<T>::type;
+  // K3 reads the caller's planes (their y type) or the f64 planes K1 wrote
+  using YT = typename std::conditional<is_yev<T>::value, typename yev_y<T>::type, double>::type;
   if constexpr (is_yev<T>::value) {
     p.ysrc = (const char *)a.obs;
     p.evsrc = p.ysrc + yev_ev_offset(a.B, a.T, a.n, sizeof(YT));
