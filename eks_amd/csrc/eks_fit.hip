@@ -505,6 +505,10 @@ constexpr long long kSelSplitB = 512;
 long long g_fit_select = 0;
 namespace {
 constexpr long long kSegKeys = 1024;
+// the split path's top digit: 14 bits (exponent + 3 mantissa bits; 64 KB LDS
+// histograms): a 4x narrower bin than k_fit_select's 12 bits, so k_sel_final
+// selects among ~4x fewer candidates (config 2: ~18 k -> ~4.5 k keys)
+constexpr int kSplitBits = 14, kSplitBins = 1 << kSplitBits, kSplitLo = 63 - kSplitBits;
 
 struct SelRow {  // per-row state of the split selection (zeroed by a memset)
   unsigned nan, ncand;
@@ -514,23 +518,23 @@ struct SelRow {  // per-row state of the split selection (zeroed by a memset)
 __global__ __launch_bounds__(256) void k_sel_hist(const double *__restrict__ worst, long long TT,
                                                   int G, unsigned *__restrict__ ghist,
                                                   SelRow *__restrict__ rows) {
-  __shared__ unsigned hist[kBins];
-  constexpr int lo_bit = 51;
+  __shared__ unsigned hist[kSplitBins];
+  constexpr int lo_bit = kSplitLo;
   const long long b = blockIdx.x / G, g = blockIdx.x % G;
   const uint64_t *keys = reinterpret_cast<const uint64_t *>(worst + b * TT);
   const long long k0 = g * kSegKeys, k1 = k0 + kSegKeys < TT ? k0 + kSegKeys : TT;
-  for (int i = threadIdx.x; i < kBins; i += 256) hist[i] = 0;
+  for (int i = threadIdx.x; i < kSplitBins; i += 256) hist[i] = 0;
   __syncthreads();
   bool nan = false;
   for (long long i = k0 + threadIdx.x; i < k1; i += 256) {
     const uint64_t x = keys[i];
     nan |= (x & 0x7fffffffffffffffull) > 0x7ff0000000000000ull;
-    atomicAdd(&hist[(unsigned)(x >> lo_bit) & (kBins - 1)], 1u);
+    atomicAdd(&hist[(unsigned)(x >> lo_bit) & (kSplitBins - 1)], 1u);
   }
   if (__any(nan) && (threadIdx.x & 63) == 0) atomicOr(&rows[b].nan, 1u);
   __syncthreads();
-  unsigned *gh = ghist + b * kBins;
-  for (int i = threadIdx.x; i < kBins; i += 256)
+  unsigned *gh = ghist + b * kSplitBins;
+  for (int i = threadIdx.x; i < kSplitBins; i += 256)
     if (hist[i]) atomicAdd(&gh[i], hist[i]);
 }
 
@@ -538,8 +542,8 @@ __global__ __launch_bounds__(256) void k_sel_bin(const unsigned *__restrict__ gh
                                                  SelRow *__restrict__ rows) {
   __shared__ long long si[2 + 4];
   const long long b = blockIdx.x;
-  const unsigned *h = ghist + b * kBins;
-  constexpr unsigned per = kBins / 256;
+  const unsigned *h = ghist + b * kSplitBins;
+  constexpr unsigned per = kSplitBins / 256;
   long long mine = 0;
   for (unsigned d = threadIdx.x * per; d < (threadIdx.x + 1) * per; ++d) mine += h[d];
   long long total;
@@ -547,7 +551,7 @@ __global__ __launch_bounds__(256) void k_sel_bin(const unsigned *__restrict__ gh
   if (lo >= acc && lo < acc + mine) {  // exactly one thread
     unsigned d = threadIdx.x * per;
     while (acc + h[d] <= (unsigned long long)lo) acc += h[d++];
-    rows[b].binpfx = (unsigned long long)d << 51;
+    rows[b].binpfx = (unsigned long long)d << kSplitLo;
     rows[b].kin = lo - acc;
     rows[b].cnt_bin = h[d];
   }
@@ -567,7 +571,7 @@ __global__ __launch_bounds__(256) void k_sel_cand(const double *__restrict__ wor
   const long long k0 = g * kSegKeys, k1 = k0 + kSegKeys < TT ? k0 + kSegKeys : TT;
   SelRow &row = rows[b];
   const bool nan = row.nan != 0;
-  const uint64_t binpfx = row.binpfx, binmask = ~((1ull << 51) - 1);
+  const uint64_t binpfx = row.binpfx, binmask = ~((1ull << kSplitLo) - 1);
   uint64_t *krow = kept ? kept + b * W : nullptr;
   uint64_t *ck = ckey + b * TT;
   unsigned *ci = cidx + b * TT;
@@ -650,7 +654,7 @@ __global__ __launch_bounds__(BLK) void k_sel_final(const double *__restrict__ wo
   const long long kin = (long long)row.kin, cnt = (long long)row.cnt_bin;
   const uint64_t *ck = ckey + b * TT;
   const unsigned *ci = cidx + b * TT;
-  constexpr int lo_bit = 51;
+  constexpr int lo_bit = kSplitLo;
   uint64_t ka;
   const uint64_t *src = ck;
   if (cnt <= kCandBig) {
@@ -695,10 +699,25 @@ __global__ __launch_bounds__(BLK) void k_sel_final(const double *__restrict__ wo
   const double th = sthr;
   // the bin's kept frames; keys above the bin are >= kb >= th: kept only
   // when equal to th, i.e. th == kb with kb above the bin (then the keys
-  // equal to kb, all outside the candidates, are marked from the row)
-  for (long long i = threadIdx.x; i < cnt; i += BLK)
-    if (__longlong_as_double((long long)src[i]) <= th)
-      atomicOr((unsigned long long *)&krow[ci[i] >> 6], 1ull << (ci[i] & 63));
+  // equal to kb, all outside the candidates, are marked from the row).
+  // When the row's mask fits in LDS after the candidates, the bits are
+  // gathered there (LDS atomics) and each touched word is OR-ed into the
+  // mask once, instead of one global atomic per kept frame.
+  if (src == cand && cnt + W <= kCandBig) {
+    uint64_t *lm = cand + cnt;
+    for (long long w = threadIdx.x; w < W; w += BLK) lm[w] = 0;
+    __syncthreads();
+    for (long long i = threadIdx.x; i < cnt; i += BLK)
+      if (__longlong_as_double((long long)src[i]) <= th)
+        atomicOr((unsigned long long *)&lm[ci[i] >> 6], 1ull << (ci[i] & 63));
+    __syncthreads();
+    for (long long w = threadIdx.x; w < W; w += BLK)
+      if (lm[w]) atomicOr((unsigned long long *)&krow[w], (unsigned long long)lm[w]);
+  } else {
+    for (long long i = threadIdx.x; i < cnt; i += BLK)
+      if (__longlong_as_double((long long)src[i]) <= th)
+        atomicOr((unsigned long long *)&krow[ci[i] >> 6], 1ull << (ci[i] & 63));
+  }
   const bool amb = (kb & ~((1ull << lo_bit) - 1)) != binpfx &&
                    th >= __longlong_as_double((long long)kb);
   if (amb) {
@@ -1169,7 +1188,7 @@ constexpr int kNW = 16;
 // frames: the hand-off planes' rows, B values each, are written by
 // consecutive lanes; the worst rows leave through an LDS tile) with the
 // frame's n columns reduced in a runtime loop (runtime E)
-template <typename T, typename YT>
+template <typename T, typename YT, int E>
 __global__ __launch_bounds__(256) void k_fitw_worst(const T *__restrict__ obs, FitShape sh,
                                                     long long sb, long long st, long long se,
                                                     long long sj, int Ert, int n, int median,
@@ -1191,7 +1210,7 @@ __global__ __launch_bounds__(256) void k_fitw_worst(const T *__restrict__ obs, F
     bool nan = false;
     for (int j = 0; j < n; ++j) {
       double avg, var;
-      ensemble_reduce_rt<T>(pb + t * st + j * sj, se, Ert, median != 0, avg, var);
+      column_reduce<E, T>(pb + t * st + j * sj, se, Ert, median != 0, avg, var);
       nan |= (var != var);
       v = var > v ? var : v;
       if (t == 0) ks.K[b * n + j] = avg;
@@ -1224,7 +1243,7 @@ __global__ __launch_bounds__(256) void k_fitw_worst(const T *__restrict__ obs, F
   }
 }
 
-template <typename T, typename YT, bool FROM_YEV>
+template <typename T, typename YT, bool FROM_YEV, int E>
 __global__ __launch_bounds__(256) void k_fitw_accum(const T *__restrict__ obs, FitShape sh,
                                                     long long sb, long long st, long long se,
                                                     long long sj, int Ert, int n, int median,
@@ -1258,7 +1277,7 @@ __global__ __launch_bounds__(256) void k_fitw_accum(const T *__restrict__ obs, F
       y = (double)((const YT *)yi.y)[(t * n + ic) * sh.B + b];
     } else {
       double var;
-      ensemble_reduce_rt<T>(pb + t * st, se, Ert, median != 0, y, var);
+      column_reduce<E, T>(pb + t * st, se, Ert, median != 0, y, var);
       // v = max over the group's columns, NaN if any is NaN (frame_ensemble)
       // (a NaN variance made the threshold NaN: nothing is kept either way)
       double v = var;
@@ -1469,7 +1488,7 @@ extern "C" size_t eks_fit_workspace_bytes(int64_t B, int64_t T, int n) {
   size_t bytes = (size_t)(B * T + B + B * (np + nc2) * len + B * W + B * n) * sizeof(double);
   // split selection: histograms, row states, candidate keys + indices
   if (B < kSelSplitB || g_fit_select == 2)
-    bytes += (size_t)B * kBins * 4 + (size_t)B * sizeof(SelRow) + (size_t)B * T * 12 + 256;
+    bytes += (size_t)B * kSplitBins * 4 + (size_t)B * sizeof(SelRow) + (size_t)B * T * 12 + 256;
   return bytes;
 }
 
@@ -1532,7 +1551,7 @@ extern "C" int eks_fit(const void *obs, int obs_dtype, int64_t B, int64_t T, int
   const int G = (int)((T + kSegKeys - 1) / kSegKeys);
   char *sel_base = reinterpret_cast<char *>(ks.K + B * n);
   unsigned *ghist = reinterpret_cast<unsigned *>(sel_base);
-  SelRow *rows = reinterpret_cast<SelRow *>(sel_base + (size_t)B * kBins * 4);
+  SelRow *rows = reinterpret_cast<SelRow *>(sel_base + (size_t)B * kSplitBins * 4);
   uint64_t *ckey = reinterpret_cast<uint64_t *>(
       (reinterpret_cast<uintptr_t>(rows + B) + 255) / 256 * 256);
   unsigned *cidx = reinterpret_cast<unsigned *>(ckey + B * T);
@@ -1555,7 +1574,7 @@ extern "C" int eks_fit(const void *obs, int obs_dtype, int64_t B, int64_t T, int
     prof_mark(s, "k_fit_select");
     if (split_sel) {
       // few long rows: one block per (row, segment) in four launches
-      if (hipMemsetAsync(ghist, 0, (size_t)B * kBins * 4 + (size_t)B * sizeof(SelRow), s) !=
+      if (hipMemsetAsync(ghist, 0, (size_t)B * kSplitBins * 4 + (size_t)B * sizeof(SelRow), s) !=
           hipSuccess)
         return set_err(EKS_ERR_HIP, "eks_fit: hipMemsetAsync failed");
       const unsigned gs = (unsigned)(B * G);
@@ -1604,27 +1623,28 @@ extern "C" int eks_fit(const void *obs, int obs_dtype, int64_t B, int64_t T, int
   if (n > kMaxObs) {  // 5-8 cameras: the wide kernels (runtime n, runtime E)
     if (kind != EKS_FIT_MULTICAM || r != 3)
       return set_err(EKS_ERR_UNSUPPORTED, "eks_fit: n=%d needs the PCA model with r = 3", n);
-    auto wide = [&](auto tag, auto ytag) -> int {
+    auto wide_e = [&](auto tag, auto ytag, auto Ec) -> int {
       using Tp = decltype(tag);
       using YT = decltype(ytag);
+      constexpr int EE = decltype(Ec)::value;
       prof_call_begin();
       prof_mark(s, "k_fitw_worst");
       int ncw;
       long long lcw;
       fit_chunks(B, T, ncw, lcw);  // k_fit_worst's lanes (one per (trajectory, chunk))
       const FitShape shw{B, T, ncw, lcw};
-      hipLaunchKernelGGL((k_fitw_worst<Tp, YT>), dim3(grid_for(B * (long long)ncw, 256)), dim3(256), 0, s,
+      hipLaunchKernelGGL((k_fitw_worst<Tp, YT, EE>), dim3(grid_for(B * (long long)ncw, 256)), dim3(256), 0, s,
                          (const Tp *)obs, shw, sb, st, se, sj, E, n, median, worst, yo, ks);
       int rc = check_launch("k_fitw_worst");
       if (rc || (rc = select())) return rc;
       prof_mark(s, "k_fitw_accum");
       const unsigned ga = grid_for(B * (long long)sh.NC * kNW, 256);
       if (yev)
-        hipLaunchKernelGGL((k_fitw_accum<Tp, YT, true>), dim3(ga), dim3(256), 0, s,
+        hipLaunchKernelGGL((k_fitw_accum<Tp, YT, true, 0>), dim3(ga), dim3(256), 0, s,
                            (const Tp *)obs, sh, sb, st, se, sj, E, n, median, thr, kept, W, partA,
                            yo, ks);
       else
-        hipLaunchKernelGGL((k_fitw_accum<Tp, YT, false>), dim3(ga), dim3(256), 0, s,
+        hipLaunchKernelGGL((k_fitw_accum<Tp, YT, false, EE>), dim3(ga), dim3(256), 0, s,
                            (const Tp *)obs, sh, sb, st, se, sj, E, n, median, thr, kept, W, partA,
                            yo, ks);
       if ((rc = check_launch("k_fitw_accum"))) return rc;
@@ -1635,6 +1655,14 @@ extern "C" int eks_fit(const void *obs, int obs_dtype, int64_t B, int64_t T, int
                          smooth_param, params, status);
       prof_call_end(s);
       return check_launch("k_fitw_final");
+    };
+    auto wide = [&](auto tag, auto ytag) -> int {
+      switch (E) {
+        case 3: return wide_e(tag, ytag, ic<3>{});
+        case 4: return wide_e(tag, ytag, ic<4>{});
+        case 5: return wide_e(tag, ytag, ic<5>{});
+        default: return wide_e(tag, ytag, ic<0>{});
+      }
     };
     if (y32) return wide(float{}, float{});
     return obs_dtype == EKS_F32 ? wide(float{}, double{}) : wide(double{}, double{});

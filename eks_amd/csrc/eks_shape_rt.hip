@@ -62,7 +62,7 @@ EKS_DEV void project_rt(double *out, long long oj, const double *C, const double
   }
 }
 
-template <int R, typename T>
+template <int R, typename T, int E>
 __global__ __launch_bounds__(64) void k_smooth_seq_rt(SmoothArgs a) {
   constexpr int K = R + Sym<R>::len;
   const long long b = blockIdx.x * (long long)blockDim.x + threadIdx.x;
@@ -95,7 +95,7 @@ __global__ __launch_bounds__(64) void k_smooth_seq_rt(SmoothArgs a) {
         avg = (double)ob[(t * n + j) * B + b];
         var = evp[(t * n + j) * B + b];
       } else {
-        ensemble_reduce_rt<YT>(ob + t * a.st + j * a.sj, a.se, a.E, median, avg, var);
+        column_reduce<E, YT>(ob + t * a.st + j * a.sj, a.se, a.E, median, avg, var);
       }
       kf_update_row_rt<R>(m, P, C + j * R, avg - off[j], var, acc, ok);
     }
@@ -156,7 +156,7 @@ EKS_DEV void load_row(const double *c, double (&cr)[R]) {
   for (int k = 0; k < R; ++k) cr[k] = c[k];
 }
 
-template <int R, typename T>
+template <int R, typename T, int E>
 __global__ __launch_bounds__(kBlock) void k_rt_c1(SmoothArgs a, ChunkPlan p) {
   zero_scan_sync(a, p);
   Lane<false> ln;
@@ -199,7 +199,7 @@ __global__ __launch_bounds__(kBlock) void k_rt_c1(SmoothArgs a, ChunkPlan p) {
         avg = (double)pl((const YT *)p.ysrc, t * n + j, B, b);
         var = pl((const double *)p.evsrc, t * n + j, B, b);
       } else {
-        ensemble_reduce_rt<YT>(ob + t * a.st + j * a.sj, a.se, a.E, median, avg, var);
+        column_reduce<E, YT>(ob + t * a.st + j * a.sj, a.se, a.E, median, avg, var);
         pl(ybuf, t * n + j, B, b) = avg;
         pl(evbuf, t * n + j, B, b) = var;
       }
@@ -379,8 +379,16 @@ int launch_rt_chunked(const SmoothArgs &a) {
   int rc;
   prof_call_begin();
   prof_mark(a.stream, "k_rt_c1");
-  hipLaunchKernelGGL((k_rt_c1<R, T>), dim3(gch), dim3(kBlock), 0, a.stream, a, p);
-  if ((rc = check_launch("k_rt_c1"))) return rc;
+  auto k1 = [&](auto Ec) {
+    constexpr int EE = decltype(Ec)::value;
+    hipLaunchKernelGGL((k_rt_c1<R, T, EE>), dim3(gch), dim3(kBlock), 0, a.stream, a, p);
+    return check_launch("k_rt_c1");
+  };
+  if constexpr (is_yev<T>::value)
+    rc = k1(ic<0>{});  // the members are not read: E does not matter
+  else
+    rc = dispatch_members_c(a.E, k1);
+  if (rc) return rc;
   prof_mark(a.stream, "k_c2_fscan");
   if (!wave_scan)
     hipLaunchKernelGGL((k_c2_fscan<R, 0>), dim3(g64), dim3(64), 0, a.stream, a, p);
@@ -420,10 +428,19 @@ int launch_rt(const SmoothArgs &a) {
     if (chunked) return launch_rt_chunked<R, T>(a);
     prof_call_begin();
     prof_mark(a.stream, "k_smooth_seq_rt");
-    hipLaunchKernelGGL((k_smooth_seq_rt<R, T>), dim3(grid_for(a.B, 64)), dim3(64), 0, a.stream,
-                       a);
+    auto k = [&](auto Ec) {
+      constexpr int EE = decltype(Ec)::value;
+      hipLaunchKernelGGL((k_smooth_seq_rt<R, T, EE>), dim3(grid_for(a.B, 64)), dim3(64), 0,
+                         a.stream, a);
+      return check_launch("k_smooth_seq_rt");
+    };
+    int rc;
+    if constexpr (is_yev<T>::value)
+      rc = k(ic<0>{});
+    else
+      rc = dispatch_members_c(a.E, k);
     prof_call_end(a.stream);
-    return check_launch("k_smooth_seq_rt");
+    return rc;
   };
   auto by_type = [&](auto rtag) -> int {
     switch (a.dtype) {

@@ -192,4 +192,21 @@ EKS_DEV void ensemble_reduce_rt(const T *p, long long se, int E, bool median, do
   }
 }
 
+// One coordinate's ensemble from memory (members se apart): the compiled-E
+// reduction on registers when E > 0, else the runtime-E one.  The
+// runtime-n kernels use it so that the common member counts (3, 4, 5) do not
+// pay the runtime reduction's O(E^2) memory reads.
+template <int E, typename T>
+EKS_DEV void column_reduce(const T *p, long long se, int Ert, bool median, double &avg,
+                           double &var) {
+  if constexpr (E > 0) {
+    T raw[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) raw[e] = p[(long long)e * se];
+    ensemble_reduce<E, T>(raw, median, avg, var);
+  } else {
+    ensemble_reduce_rt<T>(p, se, Ert, median, avg, var);
+  }
+}
+
 }  // namespace eks

@@ -107,12 +107,13 @@ def test_mask_long_rows_whole_row_pass(torch):
     _vs_host(st, p, 25.0)
 
 
-@pytest.mark.parametrize("T,big", [(40000, 4096), (160000, 19968)])
-def test_mask_bin_larger_than_lds(torch, T, big):
+@pytest.mark.parametrize("T,big,shift", [(40000, 4096, 51), (400000, 19968, 49)])
+def test_mask_bin_larger_than_lds(torch, T, big, shift):
     """No outliers and long rows: the threshold's top-digit bin holds more
-    frames than the LDS candidate buffer (3 072 for one block per row, 19 968
-    for the split selection's final block), so the select runs over the
-    global row / candidate buffer and the mask comes from the whole-row pass."""
+    frames than the LDS candidate buffer (3 072 for one block per row with
+    12-bit digits, 19 968 for the split selection's final block with 14-bit
+    digits), so the select runs over the global row / candidate buffer and
+    the mask comes from the whole-row pass."""
     from eks_amd import synthetic
     from eks_amd.core import ensemble_array
     rng = np.random.default_rng(20000 + T)
@@ -120,7 +121,7 @@ def test_mask_bin_larger_than_lds(torch, T, big):
     st = np.stack([synthetic.singleview_obs(rng, 5, T, outlier_frac=0.0)[:, :, 0]
                    for _ in range(3)])
     v = np.sort(ensemble_array(st[0].astype(np.float64))[1].max(axis=1))
-    key = v.view(np.uint64) >> 51
+    key = v.view(np.uint64) >> shift
     assert (key == key[int((T - 1) * q / 100)]).sum() > big
     p = _fit_both(torch, st, q)
     _vs_host(st, p, q)
