@@ -761,6 +761,25 @@ constexpr int bwd_lds_doubles() {
   return lds_steps3(R, N) * (R + Sym<R>::len) * 64 * kWV + (kWV - 1) * (R * R + R) * 64;
 }
 
+// an empty use of the model registers a later loop reads (see k3_bwd_run)
+template <int R, int N, int AI, int CI>
+EKS_DEV void touch_model(Model<R, N> &md) {
+#pragma unroll
+  for (int j = 0; j < N; ++j) asm volatile("" : "+v"(md.off[j]));
+#pragma unroll
+  for (int i = 0; i < R; ++i)
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      asm volatile("" : "+v"(md.Q[i][k]));
+      if constexpr (AI != kAId) asm volatile("" : "+v"(md.A[i][k]));
+    }
+  if constexpr (CI != kCId)
+#pragma unroll
+    for (int j = 0; j < N; ++j)
+#pragma unroll
+      for (int k = 0; k < R; ++k) asm volatile("" : "+v"(md.C[j][k]));
+}
+
 // The k3_bwd units of consecutive tickets from t on (a run ends at the first
 // ticket that is not a k3_bwd unit, which is returned).  FUSED: each wave
 // first waits for the k3_fwd unit that stored its fine chunk's start state.
@@ -901,6 +920,12 @@ EKS_DEV unsigned k3_bwd_run(const SmoothArgs &a, const Plan3 &p, const Sched3 &s
         }
       }
       if (NLL && lane_ok) pl((double *)(a.ws + p.nllp_off), f, B, b) = acc.value((double)(e - s) * N);
+      // the model registers the backward sweep reads (offsets; Q, A, C when
+      // not the identity) marked complete here, on every path: otherwise the
+      // waitcnt pass, merging the paths around each `if (tt < e)`, re-waits
+      // for their loads at every emitted step -- vmcnt counts the output
+      // stores too, so each step waited for the previous step's store
+      touch_model<R, N, AI, CI>(md);
       if (!lane_ok) {
         ok = true;
         Mp.set_identity();
