@@ -505,6 +505,10 @@ constexpr long long kSelSplitB = 512;
 long long g_fit_select = 0;
 namespace {
 constexpr long long kSegKeys = 1024;
+// k_sel_hist's segments: 8 x longer, because each block zeroes and flushes
+// a 16 384-bin LDS histogram (at 1 024 keys per block that cost 3x the keys:
+// config 2 k_sel_hist 0.010 -> 0.033 ms with the 14-bit digit)
+constexpr long long kHistSeg = 8192;
 // the split path's top digit: 14 bits (exponent + 3 mantissa bits; 64 KB LDS
 // histograms): a 4x narrower bin than k_fit_select's 12 bits, so k_sel_final
 // selects among ~4x fewer candidates (config 2: ~18 k -> ~4.5 k keys)
@@ -522,14 +526,21 @@ __global__ __launch_bounds__(256) void k_sel_hist(const double *__restrict__ wor
   constexpr int lo_bit = kSplitLo;
   const long long b = blockIdx.x / G, g = blockIdx.x % G;
   const uint64_t *keys = reinterpret_cast<const uint64_t *>(worst + b * TT);
-  const long long k0 = g * kSegKeys, k1 = k0 + kSegKeys < TT ? k0 + kSegKeys : TT;
+  const long long k0 = g * kHistSeg, k1 = k0 + kHistSeg < TT ? k0 + kHistSeg : TT;
   for (int i = threadIdx.x; i < kSplitBins; i += 256) hist[i] = 0;
   __syncthreads();
   bool nan = false;
-  for (long long i = k0 + threadIdx.x; i < k1; i += 256) {
-    const uint64_t x = keys[i];
-    nan |= (x & 0x7fffffffffffffffull) > 0x7ff0000000000000ull;
-    atomicAdd(&hist[(unsigned)(x >> lo_bit) & (kSplitBins - 1)], 1u);
+  constexpr int U = 8;  // independent key loads in flight per thread
+  for (long long i0 = k0 + threadIdx.x; i0 < k1; i0 += 256 * U) {
+    uint64_t x[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) x[u] = i0 + u * 256 < k1 ? keys[i0 + u * 256] : 0ull;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (i0 + u * 256 < k1) {
+        nan |= (x[u] & 0x7fffffffffffffffull) > 0x7ff0000000000000ull;
+        atomicAdd(&hist[(unsigned)(x[u] >> lo_bit) & (kSplitBins - 1)], 1u);
+      }
   }
   if (__any(nan) && (threadIdx.x & 63) == 0) atomicOr(&rows[b].nan, 1u);
   __syncthreads();
@@ -1579,7 +1590,9 @@ extern "C" int eks_fit(const void *obs, int obs_dtype, int64_t B, int64_t T, int
         return set_err(EKS_ERR_HIP, "eks_fit: hipMemsetAsync failed");
       const unsigned gs = (unsigned)(B * G);
       prof_mark(s, "k_sel_hist");
-      hipLaunchKernelGGL(k_sel_hist, dim3(gs), dim3(256), 0, s, worst, T, G, ghist, rows);
+      const int GH = (int)((T + kHistSeg - 1) / kHistSeg);
+      hipLaunchKernelGGL(k_sel_hist, dim3((unsigned)(B * GH)), dim3(256), 0, s, worst, T, GH,
+                         ghist, rows);
       prof_mark(s, "k_sel_bin");
       hipLaunchKernelGGL(k_sel_bin, dim3((unsigned)B), dim3(256), 0, s, ghist, lo, rows);
       prof_mark(s, "k_sel_cand");

@@ -156,6 +156,62 @@ EKS_DEV void load_row(const double *c, double (&cr)[R]) {
   for (int k = 0; k < R; ++k) cr[k] = c[k];
 }
 
+// The chunk's (step, column) pairs as one flattened stream with the loads
+// of the next DP columns in flight: the column's observation (members or
+// plane values) and its row of C with the offset.  One lane walks one
+// trajectory's chunk sequentially, so without this every column paid a full
+// load latency (n = 12: 12 round trips per step).  fetch(k, t, j) loads
+// column (t, j) into ring slot k (indices clamped into the chunk: a cache-hit
+// re-read past its end keeps the loads unconditional); col(k, t, j) consumes
+// slot k; begin(t) / end(t) bracket each step.
+constexpr int kRtDP = 4;
+template <typename Fetch, typename Col, typename Begin, typename End>
+EKS_DEV void rt_columns(long long s, long long e, int n, Fetch &&fetch, Col &&col, Begin &&begin,
+                        End &&end) {
+  constexpr int DP = kRtDP;
+  const long long Q = (e - s) * n;
+  long long tf = s;  // next column to fetch: (tf, jf)
+  int jf = 0;
+  auto fetch_next = [&](int k) {
+    if (tf < e) fetch(k, tf, jf);
+    else fetch(k, e - 1, n - 1);
+    if (++jf == n) {
+      jf = 0;
+      ++tf;
+    }
+  };
+#pragma unroll
+  for (int k = 0; k < DP; ++k) fetch_next(k);
+  long long t = s;
+  int j = 0;
+  for (long long q = 0; q < Q; q += DP) {
+#pragma unroll
+    for (int k = 0; k < DP; ++k) {
+      if (q + k < Q) {
+        if (j == 0) begin(t);
+        col(k, t, j);  // consumes slot k
+        fetch_next(k);
+        if (++j == n) {
+          j = 0;
+          end(t);
+          ++t;
+        }
+      }
+    }
+  }
+}
+
+// ring of the columns' model rows (c_j, offset_j)
+template <int R>
+struct RowRing {
+  double c[kRtDP][R], o[kRtDP];
+  EKS_DEV void fetch(int k, const double *C, const double *off, int j) {
+#pragma unroll
+    for (int u = 0; u < R; ++u) c[k][u] = C[j * R + u];
+    o[k] = off[j];
+  }
+};
+
 template <int R, typename T, int E>
 __global__ __launch_bounds__(kBlock) void k_rt_c1(SmoothArgs a, ChunkPlan p) {
   zero_scan_sync(a, p);
@@ -187,29 +243,63 @@ __global__ __launch_bounds__(kBlock) void k_rt_c1(SmoothArgs a, ChunkPlan p) {
     load_mat<R, R>(pp + L::S0, P);
   }
   NllAcc acc;
-  for (long long t = s; t < e; ++t) {
+  auto begin = [&](long long t) {
     if (first) {
       if (t > 0) kf_predict<R, kAGen>(m, P, A, Q);
     } else {
       elem_predict<R, kAGen>(El, A, Q);
     }
-    for (int j = 0; j < n; ++j) {
-      double avg, var, cr[R];
+  };
+  auto end = [&](long long) { acc.renorm(); };
+  auto absorb = [&](const double (&cr)[R], double y, double var) {
+    if (first)
+      kf_update_row_rt<R>(m, P, cr, y, var, acc, ok);
+    else
+      absorb_gen_row<R>(El, cr, y, var, ok, &acc);
+  };
+  RowRing<R> rr;
+  if constexpr (kYev || E > 0) {
+    constexpr int EE = E > 0 ? E : 1;
+    YT mr[kRtDP][EE];        // members (member input)
+    YT yr[kRtDP];            // plane values (y / ev input)
+    double er[kRtDP];
+    auto fetch = [&](int k, long long t, int j) {
+      rr.fetch(k, C, off, j);
       if constexpr (kYev) {
-        avg = (double)pl((const YT *)p.ysrc, t * n + j, B, b);
-        var = pl((const double *)p.evsrc, t * n + j, B, b);
+        yr[k] = pl((const YT *)p.ysrc, t * n + j, B, b);
+        er[k] = pl((const double *)p.evsrc, t * n + j, B, b);
       } else {
-        column_reduce<E, YT>(ob + t * a.st + j * a.sj, a.se, a.E, median, avg, var);
+        const YT *pc = ob + t * a.st + j * a.sj;
+#pragma unroll
+        for (int u = 0; u < EE; ++u) mr[k][u] = pc[(long long)u * a.se];
+      }
+    };
+    auto col = [&](int k, long long t, int j) {
+      double avg, var;
+      if constexpr (kYev) {
+        avg = (double)yr[k];
+        var = er[k];
+      } else {
+        ensemble_reduce<EE, YT>(mr[k], median, avg, var);
         pl(ybuf, t * n + j, B, b) = avg;
         pl(evbuf, t * n + j, B, b) = var;
       }
-      load_row<R>(C + j * R, cr);
-      if (first)
-        kf_update_row_rt<R>(m, P, cr, avg - off[j], var, acc, ok);
-      else
-        absorb_gen_row<R>(El, cr, avg - off[j], var, ok, &acc);
+      absorb(rr.c[k], avg - rr.o[k], var);
+    };
+    rt_columns(s, e, n, fetch, col, begin, end);
+  } else {  // runtime E: no member ring
+    for (long long t = s; t < e; ++t) {
+      begin(t);
+      for (int j = 0; j < n; ++j) {
+        double avg, var, cr[R];
+        column_reduce<0, YT>(ob + t * a.st + j * a.sj, a.se, a.E, median, avg, var);
+        pl(ybuf, t * n + j, B, b) = avg;
+        pl(evbuf, t * n + j, B, b) = var;
+        load_row<R>(C + j * R, cr);
+        absorb(cr, avg - off[j], var);
+      }
+      end(t);
     }
-    acc.renorm();
   }
   if (first) {  // the filtered state (Ab = 0), as c1_chunk
 #pragma unroll
@@ -255,16 +345,23 @@ __global__ __launch_bounds__(kBlock) void k_rt_c3(SmoothArgs a, ChunkPlan p) {
   const long long s = c * p.L, e = min(TT, s + p.L);
   bool ok = true;
   NllAcc acc;
-  for (long long t = s; t < e; ++t) {
+  RowRing<R> rr;
+  YT yr[kRtDP];
+  double er[kRtDP];
+  auto fetch = [&](int k, long long t, int j) {
+    rr.fetch(k, C, off, j);
+    yr[k] = pl(ybuf, t * n + j, B, b);
+    er[k] = pl(evbuf, t * n + j, B, b);
+  };
+  auto col = [&](int k, long long, int) {
+    kf_update_row_rt<R>(m, P, rr.c[k], (double)yr[k] - rr.o[k], er[k], acc, ok);
+  };
+  auto begin = [&](long long t) {
     if (t > 0) kf_predict<R, kAGen>(m, P, A, Q);
-    for (int j = 0; j < n; ++j) {
-      double cr[R];
-      load_row<R>(C + j * R, cr);
-      kf_update_row_rt<R>(m, P, cr, (double)pl(ybuf, t * n + j, B, b) - off[j],
-                          pl(evbuf, t * n + j, B, b), acc, ok);
-    }
+  };
+  auto end = [&](long long t) {
     acc.renorm();
-    if (!p.smooth) continue;
+    if (!p.smooth) return;
     double J[R][R], d[R];
     if (t + 1 < TT) {
       ok = rts_gain<R, kAGen>(m, P, A, Q, J, d) && ok;
@@ -290,7 +387,8 @@ __global__ __launch_bounds__(kBlock) void k_rt_c3(SmoothArgs a, ChunkPlan p) {
     for (int i = 0; i < R; ++i)
 #pragma unroll
       for (int k = 0; k < R; ++k) G[i][k] = GJ[i][k];
-  }
+  };
+  rt_columns(s, e, n, fetch, col, begin, end);
   pl((double *)(a.ws + p.nllp_off), c, B, b) = acc.value((double)(e - s) * n);
   if (!ok) flag(a.status, b, EKS_STATUS_SINGULAR);
   if (!p.smooth) return;

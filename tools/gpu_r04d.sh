@@ -14,4 +14,4 @@ print("c", sys.argv[2], "smooth ms", round(d["ms_per_step"], 4), r(d["roofline"]
 print("   e2e", round(d["end_to_end"]["ms_per_step"], 4), r(d["end_to_end"]["kernels_ms"]))
 PY
 done
-TAG=vard LIBS="default exp/varD3/libeks_hip.so exp/varD4/libeks_hip.so" VIDEOS="1024 128" bash tools/gpu_ab.sh
+TAG=vard LIBS="default exp/r03/libeks_hip.so exp/varD3/libeks_hip.so" VIDEOS="1024 256 128" bash tools/gpu_ab.sh
