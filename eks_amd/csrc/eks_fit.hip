@@ -105,6 +105,18 @@ struct FitShift {
   double *K;
 };
 
+// words the worst pass zeroes on the side (the split selection's histograms
+// and row states: no memset launch before k_sel_hist)
+struct ZeroSpan {
+  unsigned *p = nullptr;
+  long long n = 0;
+  EKS_DEV void run() const {
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+         i += (long long)gridDim.x * blockDim.x)
+      p[i] = 0u;
+  }
+};
+
 constexpr int kTile = 16;  // frames per register tile: one 128-byte row segment per lane
 
 template <int E, int N, typename T, typename YT>
@@ -112,7 +124,8 @@ __global__ __launch_bounds__(256) void k_fit_worst(const T *__restrict__ obs, Fi
                                                    long long sb, long long st, long long se,
                                                    long long sj, int Ert, int median,
                                                    double *__restrict__ worst, YevOut yo,
-                                                   FitShift ks) {
+                                                   FitShift ks, ZeroSpan zs) {
+  zs.run();
   // each lane computes kTile consecutive frames of its (trajectory, chunk)
   // into LDS; the block then writes the trajectory-major rows as whole
   // 128-byte segments (16 lanes per segment) instead of one 8-byte store
@@ -551,9 +564,20 @@ __global__ __launch_bounds__(256) void k_sel_hist(const double *__restrict__ wor
 
 __global__ __launch_bounds__(256) void k_sel_bin(const unsigned *__restrict__ ghist, long long lo,
                                                  SelRow *__restrict__ rows) {
+  // the row's histogram staged in LDS with 16-byte loads (all in flight at
+  // once), then per-thread sums, a block scan and the owner's walk in LDS
+  __shared__ uint4 hs[kSplitBins / 4];
   __shared__ long long si[2 + 4];
   const long long b = blockIdx.x;
-  const unsigned *h = ghist + b * kSplitBins;
+  const uint4 *h4 = reinterpret_cast<const uint4 *>(ghist + b * kSplitBins);
+  constexpr int per4 = kSplitBins / 4 / 256;
+  uint4 v[per4];
+#pragma unroll
+  for (int k = 0; k < per4; ++k) v[k] = h4[k * 256 + threadIdx.x];
+#pragma unroll
+  for (int k = 0; k < per4; ++k) hs[k * 256 + threadIdx.x] = v[k];
+  __syncthreads();
+  const unsigned *h = reinterpret_cast<const unsigned *>(hs);
   constexpr unsigned per = kSplitBins / 256;
   long long mine = 0;
   for (unsigned d = threadIdx.x * per; d < (threadIdx.x + 1) * per; ++d) mine += h[d];
@@ -1204,7 +1228,8 @@ __global__ __launch_bounds__(256) void k_fitw_worst(const T *__restrict__ obs, F
                                                     long long sb, long long st, long long se,
                                                     long long sj, int Ert, int n, int median,
                                                     double *__restrict__ worst, YevOut yo,
-                                                    FitShift ks) {
+                                                    FitShift ks, ZeroSpan zs) {
+  zs.run();
   __shared__ double tile[256][kTile + 1];
   __shared__ long long base[256];
   const long long lane = blockIdx.x * (long long)blockDim.x + threadIdx.x;
@@ -1499,7 +1524,7 @@ extern "C" size_t eks_fit_workspace_bytes(int64_t B, int64_t T, int n) {
   size_t bytes = (size_t)(B * T + B + B * (np + nc2) * len + B * W + B * n) * sizeof(double);
   // split selection: histograms, row states, candidate keys + indices
   if (B < kSelSplitB || g_fit_select == 2)
-    bytes += (size_t)B * kSplitBins * 4 + (size_t)B * sizeof(SelRow) + (size_t)B * T * 12 + 256;
+    bytes += (size_t)B * kSplitBins * 4 + (size_t)B * sizeof(SelRow) + (size_t)B * T * 12 + 512;
   return bytes;
 }
 
@@ -1560,7 +1585,8 @@ extern "C" int eks_fit(const void *obs, int obs_dtype, int64_t B, int64_t T, int
   // split selection (few rows): its buffers after the shifts
   const bool split_sel = g_fit_select == 1 ? false : g_fit_select == 2 ? true : B < kSelSplitB;
   const int G = (int)((T + kSegKeys - 1) / kSegKeys);
-  char *sel_base = reinterpret_cast<char *>(ks.K + B * n);
+  char *sel_base = reinterpret_cast<char *>(
+      (reinterpret_cast<uintptr_t>(ks.K + B * n) + 255) / 256 * 256);  // 16-byte loads in k_sel_bin
   unsigned *ghist = reinterpret_cast<unsigned *>(sel_base);
   SelRow *rows = reinterpret_cast<SelRow *>(sel_base + (size_t)B * kSplitBins * 4);
   uint64_t *ckey = reinterpret_cast<uint64_t *>(
@@ -1579,15 +1605,18 @@ extern "C" int eks_fit(const void *obs, int obs_dtype, int64_t B, int64_t T, int
     yo.y = yev;
     yo.ev = (double *)((char *)yev + yev_ev_offset(B, T, n, y32 ? 4 : 8));
   }
+  ZeroSpan zs;
+  if (split_sel) {
+    zs.p = ghist;
+    zs.n = (long long)(((size_t)B * kSplitBins * 4 + (size_t)B * sizeof(SelRow)) / 4);
+  }
   // the order statistics, the threshold and (with the hand-off planes
   // written) the kept-frame mask k_fit_accum reads instead of the ev plane
   auto select = [&]() -> int {
     prof_mark(s, "k_fit_select");
     if (split_sel) {
       // few long rows: one block per (row, segment) in four launches
-      if (hipMemsetAsync(ghist, 0, (size_t)B * kSplitBins * 4 + (size_t)B * sizeof(SelRow), s) !=
-          hipSuccess)
-        return set_err(EKS_ERR_HIP, "eks_fit: hipMemsetAsync failed");
+      // (ghist and the row states were zeroed by the worst pass: zs)
       const unsigned gs = (unsigned)(B * G);
       prof_mark(s, "k_sel_hist");
       const int GH = (int)((T + kHistSeg - 1) / kHistSeg);
@@ -1647,7 +1676,7 @@ extern "C" int eks_fit(const void *obs, int obs_dtype, int64_t B, int64_t T, int
       fit_chunks(B, T, ncw, lcw);  // k_fit_worst's lanes (one per (trajectory, chunk))
       const FitShape shw{B, T, ncw, lcw};
       hipLaunchKernelGGL((k_fitw_worst<Tp, YT, EE>), dim3(grid_for(B * (long long)ncw, 256)), dim3(256), 0, s,
-                         (const Tp *)obs, shw, sb, st, se, sj, E, n, median, worst, yo, ks);
+                         (const Tp *)obs, shw, sb, st, se, sj, E, n, median, worst, yo, ks, zs);
       int rc = check_launch("k_fitw_worst");
       if (rc || (rc = select())) return rc;
       prof_mark(s, "k_fitw_accum");
@@ -1698,7 +1727,7 @@ extern "C" int eks_fit(const void *obs, int obs_dtype, int64_t B, int64_t T, int
         prof_call_begin();
         prof_mark(s, "k_fit_worst");
         hipLaunchKernelGGL((k_fit_worst<EE, NN, Tp, YT>), dim3(grid), dim3(256), 0, s,
-                           (const Tp *)obs, sh, sb, st, se, sj, E, median, worst, yo, ks);
+                           (const Tp *)obs, sh, sb, st, se, sj, E, median, worst, yo, ks, zs);
         int rc = check_launch("k_fit_worst");
         if (rc) return rc;
         if ((rc = select())) return rc;
