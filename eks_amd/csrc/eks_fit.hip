@@ -620,11 +620,23 @@ __global__ __launch_bounds__(256) void k_sel_cand(const double *__restrict__ wor
   if (threadIdx.x == 0) scount = 0;
   __syncthreads();
   // whole waves per 64-key word: k0 is a multiple of 64 and every wave of the
-  // loop runs the same iterations (the index test is on the wave's last lane)
-  for (long long i0 = k0 + (threadIdx.x & ~63); i0 < k1; i0 += 256) {
+  // loop runs the same iterations (the index test is on the wave's last lane).
+  // The segment's kSegKeys / 256 keys per thread are loaded up front (all in
+  // flight at once), then classified.
+  constexpr int KP = (int)(kSegKeys / 256);
+  uint64_t xs[KP];
+#pragma unroll
+  for (int u = 0; u < KP; ++u) {
+    const long long i = k0 + (threadIdx.x & ~63) + u * 256 + (threadIdx.x & 63);
+    xs[u] = i < k1 ? keys[i] : ~0ull;
+  }
+#pragma unroll
+  for (int u = 0; u < KP; ++u) {
+    const long long i0 = k0 + (threadIdx.x & ~63) + u * 256;
+    if (i0 >= k1) break;  // wave-uniform
     const long long i = i0 + (threadIdx.x & 63);
     const bool in_row = i < k1;
-    const uint64_t x = in_row ? keys[i] : ~0ull;
+    const uint64_t x = xs[u];
     if (krow) {
       const uint64_t mb = __ballot(in_row && !nan && x < binpfx);  // below the bin: kept
       if ((threadIdx.x & 63) == 0) krow[i0 >> 6] = mb;
