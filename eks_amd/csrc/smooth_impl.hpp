@@ -750,15 +750,45 @@ __global__ __launch_bounds__(kBlock) void k_c0_shared(SmoothArgs a, ChunkPlan p)
   constexpr int EE = E > 0 ? E : 1;
   const T *pt = (const T *)a.obs + t * a.st;
   T cur[EE][N];
-  if constexpr (E > 0) load_step<E, N, T>(pt, a.se, a.sj, cur);
+  // a step's E x N members contiguous and 16-byte aligned (the pupil sweep's
+  // (T, E, 8) float32 layout): 16-byte loads, a quarter of the requests
+  constexpr bool kVec = E > 0 && (E * N) % 4 == 0 && std::is_same<T, float>::value;
+  const bool vec = kVec && a.sj == 1 && a.se == N && (((uintptr_t)a.obs | (uintptr_t)(a.st * 4)) & 15) == 0;
+  if constexpr (kVec) {
+    if (vec) {
+      float4 q[EE * N / 4];
+#pragma unroll
+      for (int k = 0; k < EE * N / 4; ++k) q[k] = reinterpret_cast<const float4 *>(pt)[k];
+#pragma unroll
+      for (int k = 0; k < EE * N / 4; ++k) {
+        const float w[4] = {q[k].x, q[k].y, q[k].z, q[k].w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) cur[(4 * k + u) / N][(4 * k + u) % N] = w[u];
+      }
+    } else {
+      load_step<E, N, T>(pt, a.se, a.sj, cur);
+    }
+  } else if constexpr (E > 0) {
+    load_step<E, N, T>(pt, a.se, a.sj, cur);
+  }
   double avg[N], rv[N];
   reduce_step<E, N, T>(cur, pt, a.se, a.sj, a.E, a.median != 0, avg, rv);
   YT *ybuf = (YT *)(a.ws + p.y_off);
   double *evbuf = (double *)(a.ws + p.ev_off);
+  if constexpr (N % 4 == 0 && std::is_same<YT, float>::value) {  // 16-byte stores
 #pragma unroll
-  for (int j = 0; j < N; ++j) {
-    ybuf[t * N + j] = (YT)avg[j];
-    evbuf[t * N + j] = rv[j];
+    for (int j = 0; j < N; j += 4)
+      *reinterpret_cast<float4 *>(ybuf + t * N + j) =
+          make_float4((float)avg[j], (float)avg[j + 1], (float)avg[j + 2], (float)avg[j + 3]);
+#pragma unroll
+    for (int j = 0; j < N; j += 2)
+      *reinterpret_cast<double2 *>(evbuf + t * N + j) = make_double2(rv[j], rv[j + 1]);
+  } else {
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      ybuf[t * N + j] = (YT)avg[j];
+      evbuf[t * N + j] = rv[j];
+    }
   }
 }
 
