@@ -784,9 +784,9 @@ EKS_DEV void touch_model(Model<R, N> &md) {
 // ticket that is not a k3_bwd unit, which is returned).  FUSED: each wave
 // first waits for the k3_fwd unit that stored its fine chunk's start state.
 // LB: the backward chain's look-back (publish the unit's maps, walk, fold).
-// Its code costs the hot loop SGPRs (spills: 21 -> 153 v_readlane in the
-// ISA, k3_bwd 1.94 -> 2.16 ms at config 4) while it only pays where few
-// groups share the chip (the 8-GPU shard: 0.365 -> 0.348 ms), so it is a
+// It only pays where few groups share the chip (the 8-GPU shard's k3_bwd:
+// 0.365 -> 0.348 ms) and adds SGPR pressure to the hot loop (21 -> 153
+// v_readlane in the ISA; config 4 measured the same either way), so it is a
 // separate instantiation, launched for small batches (a3_bwd_lookback).
 template <int R, int N, int E, typename T, int AI, int CI, bool NLL, bool FUSED, bool LB = true>
 EKS_DEV unsigned k3_bwd_run(const SmoothArgs &a, const Plan3 &p, const Sched3 &sc, unsigned t,
