@@ -272,8 +272,9 @@ int eks_newton_filter(int64_t B, int64_t T, int n, int r, const double *y, const
  * Writes params (B, eks_param_len(n, r)) for eks_smooth.  obs and strides
  * as eks_smooth (T >= 2).  status (B) or NULL: EKS_STATUS_SINGULAR where no
  * frame was kept (NaN threshold).  workspace: eks_fit_workspace_bytes.
- * n in {2, 4, 6, 8} (coordinate pairs: single view, or 2V for V <= 4
- * cameras; the multi-camera wrappers fit on the host for any V).
+ * n even, 2 <= n <= 16 (coordinate pairs: single view, or 2V for V <= 8
+ * cameras; n > 8 runs the wide kernels and needs EKS_FIT_MULTICAM with
+ * r = 3; the per-keypoint multi-camera wrappers fit on the host for any V).
  */
 enum { EKS_FIT_SINGLEVIEW = 1, EKS_FIT_MULTICAM = 2 };
 size_t eks_fit_workspace_bytes(int64_t B, int64_t T, int n);
