@@ -1253,32 +1253,60 @@ __global__ __launch_bounds__(256) void k_fitw_worst(const T *__restrict__ obs, F
     t1 = t0 + sh.Lc < sh.T ? t0 + sh.Lc : sh.T;
   }
   const T *pb = obs + b * sb;
-  auto frame = [&](long long t) {  // v_t; K and the planes as side effects
-    double v = -1.0;
-    bool nan = false;
-    for (int j = 0; j < n; ++j) {
-      double avg, var;
-      column_reduce<E, T>(pb + t * st + j * sj, se, Ert, median != 0, avg, var);
-      nan |= (var != var);
-      v = var > v ? var : v;
-      if (t == 0) ks.K[b * n + j] = avg;
-      if (yo.y) {
-        ((YT *)yo.y)[(t * n + j) * sh.B + b] = (YT)avg;
-        yo.ev[(t * n + j) * sh.B + b] = var;
+  // the frames [fa, fe) column by column (kRtDP columns' member loads in
+  // flight for compiled E); put(t, v_t) receives each frame's worst variance
+  double v = -1.0;
+  bool nan = false;
+  auto col_done = [&](long long t, int j, double avg, double var) {
+    nan |= (var != var);
+    v = var > v ? var : v;
+    if (t == 0) ks.K[b * n + j] = avg;
+    if (yo.y) {
+      ((YT *)yo.y)[(t * n + j) * sh.B + b] = (YT)avg;
+      yo.ev[(t * n + j) * sh.B + b] = var;
+    }
+  };
+  auto frames = [&](long long fa, long long fe, auto &&put) {
+    auto begin = [&](long long) {
+      v = -1.0;
+      nan = false;
+    };
+    auto end = [&](long long t) { put(t, nan ? __builtin_nan("") : v); };
+    if constexpr (E > 0) {
+      T ring[kRtDP][E];
+      auto fetch = [&](int k, long long t, int j) {
+        const T *pc = pb + t * st + j * sj;
+#pragma unroll
+        for (int u = 0; u < E; ++u) ring[k][u] = pc[u * se];
+      };
+      auto col = [&](int k, long long t, int j) {
+        double avg, var;
+        ensemble_reduce<E, T>(ring[k], median != 0, avg, var);
+        col_done(t, j, avg, var);
+      };
+      rt_columns(fa, fe, n, fetch, col, begin, end);
+    } else {
+      for (long long t = fa; t < fe; ++t) {
+        begin(t);
+        for (int j = 0; j < n; ++j) {
+          double avg, var;
+          column_reduce<0, T>(pb + t * st + j * sj, se, Ert, median != 0, avg, var);
+          col_done(t, j, avg, var);
+        }
+        end(t);
       }
     }
-    return nan ? __builtin_nan("") : v;
   };
   const long long ntiles = sh.Lc / kTile;  // Lc is a multiple of kTile
   for (long long kt = 0; kt < ntiles; ++kt) {
     const long long t = t0 + kt * kTile;
     if (active && t + kTile <= t1) {
-      for (int k = 0; k < kTile; ++k) tile[threadIdx.x][k] = frame(t + k);
+      frames(t, t + kTile, [&](long long u, double w) { tile[threadIdx.x][u - t] = w; });
       base[threadIdx.x] = b * sh.T + t;
     } else {
       base[threadIdx.x] = -1;
-      if (active)
-        for (long long u = t; u < t1; ++u) worst[b * sh.T + u] = frame(u);  // ragged end
+      if (active)  // ragged end
+        frames(t, t1, [&](long long u, double w) { worst[b * sh.T + u] = w; });
     }
     __syncthreads();
 #pragma unroll
@@ -1316,26 +1344,7 @@ __global__ __launch_bounds__(256) void k_fitw_accum(const T *__restrict__ obs, F
 #pragma unroll
   for (int j = 0; j < kNW; ++j) S2[j] = D2[j] = 0.0;
   double cnt = 0.0, npair = 0.0, S1 = 0.0, D1 = 0.0, first = 0.0, last = 0.0;
-  uint64_t kw = (FROM_YEV && t0 < t1) ? krow[t0 >> 6] : 0ull;
-  for (long long t = t0; t < t1; ++t) {
-    double y;
-    if constexpr (FROM_YEV) {
-      if ((t & 63) == 0) kw = krow[t >> 6];
-      if (!((kw >> (t & 63)) & 1ull)) continue;  // uniform over the group
-      y = (double)((const YT *)yi.y)[(t * n + ic) * sh.B + b];
-    } else {
-      double var;
-      column_reduce<E, T>(pb + t * st, se, Ert, median != 0, y, var);
-      // v = max over the group's columns, NaN if any is NaN (frame_ensemble)
-      // (a NaN variance made the threshold NaN: nothing is kept either way)
-      double v = var;
-#pragma unroll
-      for (int w = kNW / 2; w >= 1; w >>= 1) {
-        const double o = __shfl_xor(v, w, 64);
-        v = o > v ? o : v;
-      }
-      if (!(v <= th)) continue;  // uniform over the group
-    }
+  auto take = [&](double y) {  // one kept frame
     if (cnt == 0.0) {
       first = y;
     } else {
@@ -1351,6 +1360,72 @@ __global__ __launch_bounds__(256) void k_fitw_accum(const T *__restrict__ obs, F
 #pragma unroll
     for (int j = 0; j < kNW; ++j) S2[j] = fma(z, __shfl(z, base + j, 64), S2[j]);
     cnt += 1.0;
+  };
+  // a frame is kept when v = max over the group's columns <= th (uniform over
+  // the group; a NaN variance made the threshold NaN: nothing is kept)
+  auto kept_v = [&](double var) {
+    double v = var;
+#pragma unroll
+    for (int w = kNW / 2; w >= 1; w >>= 1) {
+      const double o = __shfl_xor(v, w, 64);
+      v = o > v ? o : v;
+    }
+    return v <= th;
+  };
+  // DF frames' loads in flight (unconditional, index clamped into the chunk)
+  constexpr int DF = 4;
+  auto cl = [&](long long t) { return t < t1 ? t : t1 - 1; };
+  if (t0 < t1) {
+    if constexpr (FROM_YEV) {
+      const YT *yp = (const YT *)yi.y;
+      auto ld = [&](long long t) { return yp[(cl(t) * n + ic) * sh.B + b]; };
+      YT ring[DF];
+#pragma unroll
+      for (int q = 0; q < DF; ++q) ring[q] = ld(t0 + q);
+      uint64_t kw = krow[t0 >> 6];
+      for (long long tb = t0; tb < t1; tb += DF) {
+#pragma unroll
+        for (int q = 0; q < DF; ++q) {
+          const long long t = tb + q;
+          const YT yv = ring[q];
+          ring[q] = ld(t + DF);
+          if (t < t1) {
+            if ((t & 63) == 0) kw = krow[t >> 6];
+            if ((kw >> (t & 63)) & 1ull) take((double)yv);
+          }
+        }
+      }
+    } else if constexpr (E > 0) {
+      T ring[DF][E];
+      auto ld = [&](int q, long long t) {
+        const T *pt = pb + cl(t) * st;
+#pragma unroll
+        for (int u = 0; u < E; ++u) ring[q][u] = pt[u * se];
+      };
+#pragma unroll
+      for (int q = 0; q < DF; ++q) ld(q, t0 + q);
+      for (long long tb = t0; tb < t1; tb += DF) {
+#pragma unroll
+        for (int q = 0; q < DF; ++q) {
+          const long long t = tb + q;
+          T cur[E];
+#pragma unroll
+          for (int u = 0; u < E; ++u) cur[u] = ring[q][u];
+          ld(q, t + DF);
+          if (t < t1) {
+            double y, var;
+            ensemble_reduce<E, T>(cur, median != 0, y, var);
+            if (kept_v(var)) take(y);
+          }
+        }
+      }
+    } else {
+      for (long long t = t0; t < t1; ++t) {
+        double y, var;
+        column_reduce<0, T>(pb + t * st, se, Ert, median != 0, y, var);
+        if (kept_v(var)) take(y);
+      }
+    }
   }
   const CsRt CS(n);
   double *o = part + pc * (long long)CS.kLen;

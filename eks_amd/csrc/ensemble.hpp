@@ -209,4 +209,50 @@ EKS_DEV void column_reduce(const T *p, long long se, int Ert, bool median, doubl
   }
 }
 
+// A run of (step, column) pairs -- steps [s, e), n columns each -- as one
+// flattened stream with the loads of the next DP columns in flight (the
+// runtime-n kernels: eks_shape_rt.hip, the wide fit): the column's observation (members or
+// plane values) and its row of C with the offset.  One lane walks one
+// trajectory's chunk sequentially, so without this every column paid a full
+// load latency (n = 12: 12 round trips per step).  fetch(k, t, j) loads
+// column (t, j) into ring slot k (indices clamped into the chunk: a cache-hit
+// re-read past its end keeps the loads unconditional); col(k, t, j) consumes
+// slot k; begin(t) / end(t) bracket each step.
+constexpr int kRtDP = 4;
+template <typename Fetch, typename Col, typename Begin, typename End>
+EKS_DEV void rt_columns(long long s, long long e, int n, Fetch &&fetch, Col &&col, Begin &&begin,
+                        End &&end) {
+  constexpr int DP = kRtDP;
+  const long long Q = (e - s) * n;
+  long long tf = s;  // next column to fetch: (tf, jf)
+  int jf = 0;
+  auto fetch_next = [&](int k) {
+    if (tf < e) fetch(k, tf, jf);
+    else fetch(k, e - 1, n - 1);
+    if (++jf == n) {
+      jf = 0;
+      ++tf;
+    }
+  };
+#pragma unroll
+  for (int k = 0; k < DP; ++k) fetch_next(k);
+  long long t = s;
+  int j = 0;
+  for (long long q = 0; q < Q; q += DP) {
+#pragma unroll
+    for (int k = 0; k < DP; ++k) {
+      if (q + k < Q) {
+        if (j == 0) begin(t);
+        col(k, t, j);  // consumes slot k
+        fetch_next(k);
+        if (++j == n) {
+          j = 0;
+          end(t);
+          ++t;
+        }
+      }
+    }
+  }
+}
+
 }  // namespace eks
