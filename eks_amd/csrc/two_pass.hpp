@@ -1191,8 +1191,10 @@ inline long long a3_fused_groups(const Plan3 &p) {
 
 // k3_bwd's look-back instantiation (LB): for batches of at most kLbGroups
 // 64-trajectory groups, where several time chunks of a group are resident at
-// once (eks_debug_set(EKS_DBG_A3_LB): 1 never, 2 always, 0 this rule)
-constexpr long long kLbGroups = 96;
+// once (eks_debug_set(EKS_DBG_A3_LB): 1 never, 2 always, 0 this rule).
+// Measured: 128 videos (34 groups) k3_bwd 0.336 -> 0.320 ms with it, 256
+// videos (68 groups) 0.525 -> 0.544 ms
+constexpr long long kLbGroups = 48;
 inline bool a3_bwd_lookback(const Plan3 &p) {
   if (g_a3_lb == 1) return false;
   if (g_a3_lb == 2) return true;

@@ -333,7 +333,7 @@ int eks_interp1d(const double *x, int64_t nx, const double *y, int64_t ncol, int
  *                          backward pass), 2 = one persistent launch, all
  *                          forward units first.  Results are bit-identical.
  *   EKS_DBG_A3_LB          algo 3's backward look-back: 0 = automatic (batches
- *                          of at most 96 64-trajectory groups), 1 = never,
+ *                          of at most 48 64-trajectory groups), 1 = never,
  *                          2 = always.  Results are bit-identical.
  *   EKS_DBG_RT_FORM        the runtime-n smoother (algo 4): 0 = automatic
  *                          (time-parallel when the trajectories alone do not
