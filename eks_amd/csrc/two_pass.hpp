@@ -164,12 +164,10 @@ struct MemberRing {
   }
   EKS_DEV void fetch(int slot, long long t) {
     const __amdgpu_buffer_rsrc_t rs = member_rsrc(base + t * stb);
-    // the E x N member offsets are rebuilt from the two strides at every
-    // fetch (one scalar add each) instead of being hoisted out of the step
-    // loop: ten loop-invariant offsets overflowed the SGPR file, and each
-    // load then paid a v_readlane + 4 wait states to get its offset back
-    int seb_ = seb, sjb_ = sjb;
-    asm volatile("" : "+s"(seb_), "+s"(sjb_));
+    // the E x N member offsets from the two strides (the compiler may hoist
+    // them; an empty asm that kept them per fetch -- against SGPR spills seen
+    // before the k3_bwd waitcnt fix -- measured 1.3 % slower after it)
+    const int seb_ = seb, sjb_ = sjb;
     int off_e = 0;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
