@@ -137,3 +137,25 @@ def test_model_flags_pupil_structure():
     preds = np.random.default_rng(0).normal(50, 2, size=(400, 8))
     m = fit.pupil_model(preds, np.diag([0.9, 0.99, 0.99]))
     assert batch.model_flags(m["A"], m["C"], m["Q"]) == _lib.EKS_MODEL_PUPIL
+
+
+def test_fit_sizes_and_debug_keys():
+    """eks_fit covers even n up to 16 (n > 8: the wide kernels); the debug
+    keys round-trip their values (no GPU work: host globals only)."""
+    lib = _lib.load()
+    for n in (2, 4, 8, 10, 12, 16):
+        assert lib.eks_fit_workspace_bytes(17, 5000, n) > 17 * 5000 * 8
+    assert lib.eks_fit_workspace_bytes(17, 5000, 18) == 0
+    # the wide fit's partial rows (2 + 4n + n(n + 1) doubles) are larger
+    assert lib.eks_fit_workspace_bytes(17, 5000, 16) > lib.eks_fit_workspace_bytes(17, 5000, 8)
+    for key, val in ((_lib.EKS_DBG_A3_LB, 2), (_lib.EKS_DBG_RT_FORM, 1), (_lib.EKS_DBG_FIT_SELECT, 2),
+                     (_lib.EKS_DBG_A3_MODE, 1)):
+        prev = _lib.debug_set(key, val)
+        assert _lib.debug_set(key, prev) == val
+    # the runtime-n workspace covers both forms once the time-parallel one is forced
+    prev = _lib.debug_set(_lib.EKS_DBG_RT_FORM, 2)
+    try:
+        forced = lib.eks_smooth_workspace_bytes(1 << 20, 100, 10, 3, 5, 0)
+    finally:
+        _lib.debug_set(_lib.EKS_DBG_RT_FORM, prev)
+    assert forced > lib.eks_smooth_workspace_bytes(1 << 20, 100, 10, 3, 5, 0)
