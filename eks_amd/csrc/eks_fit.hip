@@ -898,27 +898,13 @@ __global__ __launch_bounds__(256) void k_fit_accum(const T *__restrict__ obs, Fi
   double K[N];
 #pragma unroll
   for (int j = 0; j < N; ++j) K[j] = ks.K[b * N + j];
-  uint64_t kw = (FROM_YEV && t0 < t1) ? krow[t0 >> 6] : 0ull;
   double S1[N], S2[CS::kTri], D1[N], D2[CS::kTri], first[N], last[N];
   double cnt = 0.0, npair = 0.0;
 #pragma unroll
   for (int i = 0; i < N; ++i) S1[i] = D1[i] = first[i] = last[i] = 0.0;
 #pragma unroll
   for (int i = 0; i < CS::kTri; ++i) S2[i] = D2[i] = 0.0;
-  for (long long t = t0; t < t1; ++t) {
-    double y[N];
-    if constexpr (FROM_YEV) {
-      // the ensemble of this frame is already in the y plane, and whether it
-      // is kept in k_fit_select's frame mask (8 of the 24 B per frame that
-      // reading the ev plane took)
-      if ((t & 63) == 0) kw = krow[t >> 6];
-      if (!((kw >> (t & 63)) & 1ull)) continue;
-      y_of(t, y);
-    } else {
-      double v;
-      frame_ensemble<E, N, T>(pb + t * st, se, sj, Ert, median != 0, y, v);
-      if (!(v <= th)) continue;
-    }
+  auto take = [&](const double (&y)[N]) {  // one kept frame, in frame order
     if (cnt == 0.0) {
 #pragma unroll
       for (int i = 0; i < N; ++i) first[i] = y[i];
@@ -947,6 +933,46 @@ __global__ __launch_bounds__(256) void k_fit_accum(const T *__restrict__ obs, Fi
       for (int j = i; j < N; ++j) S2[tri<N>(i, j)] = fma(z[i], z[j], S2[tri<N>(i, j)]);
     }
     cnt += 1.0;
+  };
+  if constexpr (FROM_YEV) {
+    // the ensemble of every frame is already in the y plane, and whether it
+    // is kept in k_fit_select's frame mask (8 of the 24 B per frame that
+    // reading the ev plane took).  The kept frames are taken from the mask
+    // words KB at a time with their y loads in flight together (a loop over
+    // every frame with a branch per frame had one load round trip per kept
+    // frame); frame order is kept, so the sums are those of the member path.
+    constexpr int KB = 4;
+    for (long long wb = t0 & ~63LL; wb < t1; wb += 64) {
+      uint64_t m = krow[wb >> 6];
+      if (wb < t0) m &= ~0ull << (t0 - wb);
+      if (t1 - wb < 64) m &= (1ull << (t1 - wb)) - 1;
+      while (m) {
+        long long ts[KB];
+        int k = 0;
+#pragma unroll
+        for (int u = 0; u < KB; ++u) {
+          if (m) {
+            ts[u] = wb + __ffsll((long long)m) - 1;
+            m &= m - 1;
+            k = u + 1;
+          } else {
+            ts[u] = ts[0];  // padding: a cache-hit re-load, not taken
+          }
+        }
+        double ys[KB][N];
+#pragma unroll
+        for (int u = 0; u < KB; ++u) y_of(ts[u], ys[u]);
+#pragma unroll
+        for (int u = 0; u < KB; ++u)
+          if (u < k) take(ys[u]);
+      }
+    }
+  } else {
+    for (long long t = t0; t < t1; ++t) {
+      double y[N], v;
+      frame_ensemble<E, N, T>(pb + t * st, se, sj, Ert, median != 0, y, v);
+      if (v <= th) take(y);
+    }
   }
   Partial<N> pt;
   pt.cnt = cnt;
