@@ -517,7 +517,7 @@ constexpr long long kSelSplitB = 512;
 // eks_debug_set(EKS_DBG_FIT_SELECT): 0 automatic, 1 one block per row, 2 split
 long long g_fit_select = 0;
 namespace {
-constexpr long long kSegKeys = 1024;
+constexpr long long kSegKeys = 2048;
 // k_sel_hist's segments: 8 x longer, because each block zeroes and flushes
 // a 16 384-bin LDS histogram (at 1 024 keys per block that cost 3x the keys:
 // config 2 k_sel_hist 0.010 -> 0.033 ms with the 14-bit digit)
