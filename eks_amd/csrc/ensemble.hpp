@@ -109,12 +109,8 @@ template <int E, typename T>
 EKS_DEV void ensemble_reduce(const T (&raw)[E], bool median, double &avg, double &var) {
   constexpr double invE = 1.0 / (double)E, invE2 = 1.0 / ((double)E * (double)E);
   double x[E];
-  bool has_nan = false;
 #pragma unroll
-  for (int e = 0; e < E; ++e) {
-    x[e] = to_f64(raw[e]);
-    has_nan |= (raw[e] != raw[e]);
-  }
+  for (int e = 0; e < E; ++e) x[e] = to_f64(raw[e]);
   const double mean = rounded(np_sum<E>(x) * invE);
   double d[E];
 #pragma unroll
@@ -125,7 +121,18 @@ EKS_DEV void ensemble_reduce(const T (&raw)[E], bool median, double &avg, double
   var = rounded(np_sum<E>(d) * invE2);  // NaN members make it NaN by themselves
   if (median) {
     avg = median_of<E, T>(raw);
-    if (has_nan) avg = __builtin_nan("");  // the selection would skip them
+    // a NaN member makes the sum NaN, so only a NaN mean (a NaN member, or
+    // +inf and -inf members) needs the per-member test: one compare per
+    // column on the common path instead of E.  The selection would skip NaN
+    // members; np.median returns NaN.
+    const bool mnan = mean != mean;
+    if (__builtin_amdgcn_ballot_w64(mnan) != 0) {  // wave-uniform: skipped as a whole
+      asm volatile("");  // not speculated: the common path runs none of this
+      bool has_nan = false;
+#pragma unroll
+      for (int e = 0; e < E; ++e) has_nan |= (raw[e] != raw[e]);
+      if (mnan && has_nan) avg = __builtin_nan("");
+    }
   } else {
     avg = mean;
   }

@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include "eks_common.hpp"
+#include "tuning.hpp"
 
 namespace eks {
 
@@ -39,10 +40,25 @@ EKS_DEV unsigned ld_flag(const unsigned *p) {
   return __hip_atomic_load((k3_gu32 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // publish: every payload store of this wave drained, then one flag store of
-// value v (1 unless the flag has several states)
+// value v (1 unless the flag has several states).  kHandoffFences: every lane
+// issues an agent-scope release fence (its payload stores made visible at
+// agent scope before anything after the fence), then lane 0 stores the flag.
 EKS_DEV void publish_flag(unsigned *flag, int lane, unsigned v = 1u) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (kHandoffFences) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   if (lane == 0) __hip_atomic_store((k3_gu32 *)flag, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// after a poll that saw a published flag: the payload loads below it
+// (kHandoffFences: an agent-scope acquire fence; else a compiler-level one,
+// the payload being read with L1- and L2-bypassing agent-scope loads)
+EKS_DEV void acquire_after_poll() {
+  if constexpr (kHandoffFences)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  else
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 // a wall-clock deadline for one wait
@@ -68,7 +84,7 @@ EKS_DEV bool wait_flag(const unsigned *flag, long long wait_ticks, unsigned v = 
     if (dl.expired()) return false;
     __builtin_amdgcn_s_sleep(2);
   }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the payload loads below the poll
+  acquire_after_poll();  // the payload loads below the poll
   return true;
 }
 
@@ -84,7 +100,7 @@ EKS_DEV bool wait_flag_lanes(const unsigned *flag, bool need, long long wait_tic
     if (dl.expired()) return false;
     __builtin_amdgcn_s_sleep(2);
   }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  acquire_after_poll();
   return true;
 }
 
@@ -105,7 +121,7 @@ constexpr unsigned kAggReady = 1u, kIncReady = 2u;
 EKS_DEV bool inc_ready(const unsigned *flag, long long wait_ticks) {
   if (wait_ticks < 0) return false;  // fault injection: always look back
   if ((unsigned)__builtin_amdgcn_readfirstlane(ld_flag(flag)) < kIncReady) return false;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  acquire_after_poll();
   return true;
 }
 EKS_DEV long long look_back(const unsigned *flags, long long j, long long stride, int step,
@@ -128,7 +144,7 @@ EKS_DEV long long look_back(const unsigned *flags, long long j, long long stride
       const int k0 = __ffsll((long long)inc) - 1;  // the nearest inclusive value
       const unsigned long long before = k0 == 0 ? 0ull : ((1ull << k0) - 1ull);
       if ((none & before) == 0ull) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        acquire_after_poll();
         return base + (long long)step * k0;
       }
     } else if (none == 0ull && all == ~0ull) {

@@ -52,7 +52,7 @@ namespace eks {
 // debug / fault-injection settings (eks_debug_set; defined in eks_smooth_api.hip)
 extern long long g_wait_ticks;      // chain wait bound (wall_clock64 ticks), < 0: forced timeouts
 extern long long g_a3_slice_bytes;  // algo-3 member offset span per slice (0: 4 GB)
-extern long long g_a3_mode;         // algo-3 launch form (two_pass.hpp a3_fused_groups)
+extern long long g_a3_mode;         // retired key EKS_DBG_A3_MODE (round 5: one launch form)
 extern long long g_rt_form;         // runtime-n smoother form (eks_shape_rt.hip rt_chunked)
 extern long long g_a3_lb;           // k3_bwd look-back instantiation (two_pass.hpp a3_bwd_lookback)
 

@@ -24,8 +24,10 @@
 #include <c10/core/DeviceGuard.h>
 #include <torch/library.h>
 
+#include <initializer_list>
 #include <string>
 #include <tuple>
+#include <vector>
 
 #include "../../include/eks_hip.h"
 
@@ -64,6 +66,24 @@ at::TensorOptions i32(const Tensor& like) { return like.options().dtype(at::kInt
 
 Tensor contiguous_f64(const Tensor& t) { return t.to(at::kDouble).contiguous(); }
 
+// an argument of the call's device: moved there (float64, contiguous) when it
+// is a host / numpy-derived tensor, so no host pointer reaches a kernel
+Tensor on_dev_f64(const Tensor& t, const Tensor& like) {
+  return t.to(like.device(), at::kDouble).contiguous();
+}
+
+// model argument `t` must be lead + shp: per trajectory (lead = {B}) or
+// shared by every trajectory (lead = {}), as the Python shims check
+// (eks_amd/newton_eks.py: newton_filter_batch)
+void check_shape(const Tensor& t, const char* name, bool shared, int64_t B,
+                 std::initializer_list<int64_t> shp) {
+  std::vector<int64_t> want;
+  if (!shared) want.push_back(B);
+  want.insert(want.end(), shp.begin(), shp.end());
+  TORCH_CHECK(t.sizes().vec() == want, name, " has shape ", t.sizes(), ", expected ",
+              at::IntArrayRef(want));
+}
+
 // ---------------------------------------------------------------- ensemble
 std::tuple<Tensor, Tensor> ensemble_gpu(const Tensor& obs, const std::string& mode) {
   need_gpu(obs, "obs");
@@ -96,12 +116,19 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> forward_gpu(const Tensor& y, 
                                                                const Tensor& C) {
   need_gpu(y, "y");
   TORCH_CHECK(y.dim() == 3 && ev.sizes() == y.sizes(), "y and ev must both be (B, T, n)");
+  TORCH_CHECK(m0.dim() == 1 || m0.dim() == 2, "m0 must be (r,) or (B, r)");
   const c10::DeviceGuard g(y.device());
   const int64_t B = y.size(0), T = y.size(1), n = y.size(2), r = m0.size(-1);
-  const int shared = m0.dim() == 1 ? 1 : 0;
-  Tensor y_ = contiguous_f64(y), ev_ = contiguous_f64(ev);
-  Tensor m0_ = contiguous_f64(m0), S0_ = contiguous_f64(S0), A_ = contiguous_f64(A);
-  Tensor Q_ = contiguous_f64(Q), C_ = contiguous_f64(C);
+  const bool sh = m0.dim() == 1;
+  const int shared = sh ? 1 : 0;
+  check_shape(m0, "m0", sh, B, {r});
+  check_shape(S0, "S0", sh, B, {r, r});
+  check_shape(A, "A", sh, B, {r, r});
+  check_shape(Q, "Q", sh, B, {r, r});
+  check_shape(C, "C", sh, B, {n, r});
+  Tensor y_ = contiguous_f64(y), ev_ = on_dev_f64(ev, y);
+  Tensor m0_ = on_dev_f64(m0, y), S0_ = on_dev_f64(S0, y), A_ = on_dev_f64(A, y);
+  Tensor Q_ = on_dev_f64(Q, y), C_ = on_dev_f64(C, y);
   Tensor mf = at::empty({B, T, r}, f64(y));
   Tensor Vf = at::empty({B, T, r, r}, f64(y));
   Tensor S = at::empty({B, T, r, r}, f64(y));
@@ -130,11 +157,18 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> backward_gpu(const Tensor& mf, const 
                                                         const Tensor& S, const Tensor& A) {
   need_gpu(mf, "mf");
   TORCH_CHECK(mf.dim() == 3, "mf must be (B, T, r)");
+  TORCH_CHECK(A.dim() == 2 || A.dim() == 3, "A must be (r, r) or (B, r, r)");
   const c10::DeviceGuard g(mf.device());
   const int64_t B = mf.size(0), T = mf.size(1), r = mf.size(2);
-  const int shared = A.dim() == 2 ? 1 : 0;
-  Tensor mf_ = contiguous_f64(mf), Vf_ = contiguous_f64(Vf), S_ = contiguous_f64(S);
-  Tensor A_ = contiguous_f64(A);
+  const bool sh = A.dim() == 2;
+  const int shared = sh ? 1 : 0;
+  TORCH_CHECK(Vf.sizes() == at::IntArrayRef({B, T, r, r}), "Vf has shape ", Vf.sizes(),
+              ", expected (", B, ", ", T, ", ", r, ", ", r, ")");
+  TORCH_CHECK(S.sizes() == at::IntArrayRef({B, T, r, r}), "S has shape ", S.sizes(),
+              ", expected (", B, ", ", T, ", ", r, ", ", r, ")");
+  check_shape(A, "A", sh, B, {r, r});
+  Tensor mf_ = contiguous_f64(mf), Vf_ = on_dev_f64(Vf, mf), S_ = on_dev_f64(S, mf);
+  Tensor A_ = on_dev_f64(A, mf);
   Tensor ms = at::empty({B, T, r}, f64(mf));
   Tensor Vs = at::empty({B, T, r, r}, f64(mf));
   Tensor CV = at::empty({B, T > 1 ? T - 1 : 0, r, r}, f64(mf));
@@ -162,6 +196,8 @@ std::tuple<Tensor, Tensor, Tensor> smooth_impl(const Tensor& obs, const Tensor& 
                                                int64_t algo, bool want_out) {
   need_gpu(obs, "obs");
   need_gpu(params, "params");
+  TORCH_CHECK(params.device() == obs.device(), "params is on ", params.device().str(),
+              ", obs on ", obs.device().str());
   TORCH_CHECK(obs.dim() == 4 && obs.size(3) == n, "obs must be viewed as (B, T, E, n) with n=", n);
   const c10::DeviceGuard g(obs.device());
   const int64_t B = obs.size(0), T = obs.size(1), E = obs.size(2);
@@ -251,12 +287,19 @@ std::tuple<Tensor, Tensor> newton_gpu(const Tensor& y, const Tensor& ev, const T
                                       const Tensor& E, int64_t max_iter) {
   need_gpu(y, "y");
   TORCH_CHECK(y.dim() == 3 && ev.sizes() == y.sizes(), "y and ev must both be (B, T, n)");
+  TORCH_CHECK(mu0.dim() == 1 || mu0.dim() == 2, "mu0 must be (r,) or (B, r)");
   const c10::DeviceGuard g(y.device());
   const int64_t B = y.size(0), T = y.size(1), n = y.size(2), r = mu0.size(-1);
-  const int shared = mu0.dim() == 1 ? 1 : 0;
-  Tensor y_ = contiguous_f64(y), ev_ = contiguous_f64(ev), mu0_ = contiguous_f64(mu0);
-  Tensor S0_ = contiguous_f64(S0), A_ = contiguous_f64(A), B_ = contiguous_f64(Bm),
-         E_ = contiguous_f64(E);
+  const bool sh = mu0.dim() == 1;
+  const int shared = sh ? 1 : 0;
+  check_shape(mu0, "mu0", sh, B, {r});
+  check_shape(S0, "S0", sh, B, {r, r});
+  check_shape(A, "A", sh, B, {r, r});
+  check_shape(Bm, "B", sh, B, {n, r});
+  check_shape(E, "E", sh, B, {r, r});
+  Tensor y_ = contiguous_f64(y), ev_ = on_dev_f64(ev, y), mu0_ = on_dev_f64(mu0, y);
+  Tensor S0_ = on_dev_f64(S0, y), A_ = on_dev_f64(A, y), B_ = on_dev_f64(Bm, y),
+         E_ = on_dev_f64(E, y);
   Tensor q = at::empty({B, T, r}, f64(y));
   Tensor status = at::zeros({B}, i32(y));
   check(eks_newton_filter(B, T, (int)n, (int)r, y_.data_ptr<double>(), ev_.data_ptr<double>(),
@@ -279,7 +322,7 @@ Tensor interp_gpu(const Tensor& x, const Tensor& y, const Tensor& xq) {
   TORCH_CHECK(y.dim() == 2 && x.dim() == 1 && xq.dim() == 1 && y.size(0) == x.size(0),
               "x (n,), y (n, C), xq (q,)");
   const c10::DeviceGuard g(x.device());
-  Tensor x_ = contiguous_f64(x), y_ = y.to(at::kDouble), xq_ = contiguous_f64(xq);
+  Tensor x_ = contiguous_f64(x), y_ = y.to(x.device(), at::kDouble), xq_ = on_dev_f64(xq, x);
   const int64_t n = x_.size(0), C = y_.size(1), q = xq_.size(0);
   Tensor out = at::empty({q, C}, f64(x));
   Tensor status = at::zeros({q}, i32(x));

@@ -13,6 +13,17 @@ namespace eks {
 constexpr bool kNtLoad = true;
 constexpr bool kNtOut = true;
 
+// In-launch hand-offs (handoff.hpp): false = the ISA protocol (payload
+// stores write-through at agent scope, s_waitcnt vmcnt(0), flag store;
+// consumer: flag poll, compiler-level acquire, L2-bypassing payload loads);
+// true = the HIP memory model's agent-scope release / acquire fences around
+// the same accesses (buffer_wbl2 sc1 before the flag, buffer_inv sc1 after
+// the poll).  Both are measured in DESIGN.md.
+#ifndef EKS_HANDOFF_FENCES
+#define EKS_HANDOFF_FENCES 0
+#endif
+constexpr bool kHandoffFences = EKS_HANDOFF_FENCES != 0;
+
 // member prefetch distance (steps) of both algo-3 passes
 constexpr int kK3D = 2;
 

@@ -76,9 +76,6 @@ struct Plan3 {
   // sync block (zeroed every call): ticket counters (own 128-byte lines),
   // then one flag word per unit for each pass
   size_t sync_bytes = 0, flag1_off = 0, flag2_off = 0;
-  // one launch for both passes (k3_fused): per k3_fwd unit, "its fine start
-  // states are stored" (the bwd units that read them wait for it)
-  size_t flag3_off = 0;
   size_t fst_off = 0, inc2_off = 0, nllp_off = 0, prm_off = 0, total = 0;
   // look-back aggregates: k3_fwd's unit elements, k3_bwd's 4 chunk maps per unit
   size_t agg1_off = 0, agg2_off = 0;
@@ -96,8 +93,7 @@ inline Plan3 make_plan3(long long B, long long T, int r, int n) {
   p.units_f = p.NCu * p.ng;
   p.flag1_off = 256;
   p.flag2_off = p.flag1_off + (size_t)p.units_f * 4;
-  p.flag3_off = p.flag2_off + (size_t)p.units * 4;
-  p.sync_bytes = align256(p.flag3_off + (size_t)p.units_f * 4);
+  p.sync_bytes = align256(p.flag2_off + (size_t)p.units * 4);
   size_t off = p.sync_bytes;
   auto take = [&](size_t bytes) {
     const size_t o = off;
@@ -363,87 +359,38 @@ unsigned persistent_grid(long long units) {
 }
 
 // ---------------------------------------------------------------------------
-// Ticket schedules.  Separate launches (mode 0: k3_fwd, mode 1: k3_bwd): a
-// ticket is a unit, time-chunk major.  One launch for both passes (mode 2,
-// k3_fused): the tickets run F_0, F_1, B_0, F_2, B_1, ..., F_{NB-1},
-// B_{NB-2}, B_{NB-1} over batches of GB 64-trajectory groups, F_k = the
-// k3_fwd units of batch k (time-chunk major) and B_k = its k3_bwd units
-// (reverse time).  Every unit waits only for units with smaller tickets:
-// its chain neighbours, and (B_k) the F_k units that stored its fine start
-// states.  GB = ng: all forward units, then all backward ones (the backward
-// pass starts where the forward one ends, its first units re-reading the
-// members the last forward units just read); small GB: the backward pass of
-// a batch follows its forward pass one batch later, so its member re-read
-// comes (in part) from the Infinity Cache.
+// Ticket schedule of one pass (mode 0: k3_fwd, mode 1: k3_bwd): a ticket is a
+// unit, time-chunk major (k3_bwd: time chunks counted from the end), so the
+// unit a unit waits for holds a smaller ticket.  (Round 4's one-launch form
+// of both passes, k3_fused, measured no better at any size and was removed.)
 // ---------------------------------------------------------------------------
 struct Sched3 {
-  int mode = 0;  // 0 fwd only, 1 bwd only, 2 both
-  long long ng = 0, GB = 0, NB = 0, gl = 0, NCu = 0, NCc = 0;
+  int mode = 0;  // 0 fwd, 1 bwd
+  long long ng = 0, NCu = 0, NCc = 0;
 };
 struct Work3 {
   int phase;  // 0 a k3_fwd unit, 1 a k3_bwd unit, 2 none (the grid drains)
   long long c, grp;  // time chunk (k3_bwd: counted from the end), group
 };
-inline Sched3 make_sched3(const Plan3 &p, int mode, long long gb) {
+inline Sched3 make_sched3(const Plan3 &p, int mode) {
   Sched3 s;
   s.mode = mode;
   s.ng = p.ng;
-  s.GB = gb > 0 && gb < p.ng ? gb : p.ng;
-  s.NB = (p.ng + s.GB - 1) / s.GB;
-  s.gl = p.ng - (s.NB - 1) * s.GB;
   s.NCu = p.NCu;
   s.NCc = p.NCc;
   return s;
 }
-// MODE: the kernel's schedule (0 / 1: one pass, 32-bit arithmetic only; 2:
-// the one-launch schedule)
+// 32-bit arithmetic only
 template <int MODE>
 EKS_DEV Work3 decode3(const Sched3 &s, unsigned t) {
   Work3 w{2, 0, 0};
-  if constexpr (MODE != 2) {
-    const unsigned nc = (unsigned)(MODE == 0 ? s.NCu : s.NCc), ng = (unsigned)s.ng;
-    if (t < nc * ng) {
-      const unsigned c = t / ng;
-      w.phase = MODE;
-      w.c = c;
-      w.grp = t - c * ng;
-    }
-    return w;
+  const unsigned nc = (unsigned)(MODE == 0 ? s.NCu : s.NCc), ng = (unsigned)s.ng;
+  if (t < nc * ng) {
+    const unsigned c = t / ng;
+    w.phase = MODE;
+    w.c = c;
+    w.grp = t - c * ng;
   }
-  const long long tt = (long long)t;
-  auto seg = [&](int ph, long long batch, long long l) {
-    const long long gk = batch == s.NB - 1 ? s.gl : s.GB;
-    w.phase = ph;
-    w.c = l / gk;
-    w.grp = batch * s.GB + (l - w.c * gk);
-  };
-  const long long g0 = s.NB == 1 ? s.gl : s.GB;
-  if (tt < s.NCu * g0) {
-    seg(0, 0, tt);
-    return w;
-  }
-  long long r = tt - s.NCu * g0;
-  const long long P = (s.NCu + s.NCc) * s.GB;  // pair k (1 <= k <= NB-2): F_k, B_{k-1}
-  if (s.NB >= 3 && r < (s.NB - 2) * P) {
-    const long long k = 1 + r / P, q = r - (k - 1) * P;
-    if (q < s.NCu * s.GB) seg(0, k, q);
-    else seg(1, k - 1, q - s.NCu * s.GB);
-    return w;
-  }
-  if (s.NB >= 2) {
-    r -= (s.NB - 2) * P;
-    if (r < s.NCu * s.gl) {
-      seg(0, s.NB - 1, r);
-      return w;
-    }
-    r -= s.NCu * s.gl;
-    if (r < s.NCc * s.GB) {
-      seg(1, s.NB - 2, r);
-      return w;
-    }
-    r -= s.NCc * s.GB;
-  }
-  if (r < s.NCc * s.gl) seg(1, s.NB - 1, r);
   return w;
 }
 
@@ -463,15 +410,10 @@ constexpr int fwd_lds_doubles() {
   return ((fwd_fpw<R>() > 1 ? kWV : 1) + kWV) * Elem<R>::len * 64 + (R + Sym<R>::len) * 64;
 }
 
-// The k3_fwd units of consecutive tickets from t on (a run ends at the
-// first ticket that is not a k3_fwd unit, which is returned).  FUSED: the
-// fine start states are stored write-through and each unit sets its
-// flag3 word once they are (k3_fused's backward units wait for it).
-// FWD_NT: non-temporal member loads (the two-launch form and the one-launch
-// form with all forward units first: nothing re-reads them soon); the batched
-// one-launch form loads them with the default policy, so that the backward
-// units one batch later find them in the Infinity Cache.
-template <int R, int N, int E, typename T, int AI, int CI, bool FUSED, bool FWD_NT = kNtLoad>
+// The k3_fwd units of consecutive tickets from t on (the run ends when the
+// tickets run out).  Member loads are non-temporal: nothing re-reads them
+// soon (7 GB at config 4 pass through the caches before k3_bwd).
+template <int R, int N, int E, typename T, int AI, int CI>
 EKS_DEV unsigned k3_fwd_run(const SmoothArgs &a, const Plan3 &p, const Sched3 &sc, unsigned t,
                             double *lds, unsigned *tk, unsigned *ctr, int &it) {
   constexpr int EL = Elem<R>::len, KS = R + Sym<R>::len;
@@ -485,12 +427,11 @@ EKS_DEV unsigned k3_fwd_run(const SmoothArgs &a, const Plan3 &p, const Sched3 &s
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63;
   const long long B = a.B, TT = a.T;
   unsigned *flags = (unsigned *)(a.ws + p.flag1_off);
-  unsigned *done = (unsigned *)(a.ws + p.flag3_off);
   double *fst = (double *)(a.ws + p.fst_off);
   double *agg1 = (double *)(a.ws + p.agg1_off);
   const double *prm = (const double *)(a.ws + p.prm_off);
   // member ring, persists across the units of the run
-  typename SrcOf<E, N, T, D, FWD_NT>::type src;
+  typename SrcOf<E, N, T, D>::type src;
   src.init(a);
   Model<R, N> md;
   // model + the first member steps of unit wk (structure checked by
@@ -517,7 +458,7 @@ EKS_DEV unsigned k3_fwd_run(const SmoothArgs &a, const Plan3 &p, const Sched3 &s
 #pragma unroll
       for (int j = i; j < R; ++j) P[i][j] = P[j][i] = shS[k++][l];
   };
-  Work3 wk = decode3<FUSED ? 2 : 0>(sc, t);  // uniform: every index below in SGPRs
+  Work3 wk = decode3<0>(sc, t);  // uniform: every index below in SGPRs
   head(wk);
   while (wk.phase == 0) {
     unsigned tnext = 0;
@@ -606,7 +547,7 @@ EKS_DEV unsigned k3_fwd_run(const SmoothArgs &a, const Plan3 &p, const Sched3 &s
     if (threadIdx.x == 0) tk[(it + 1) & 1] = tnext;
     __syncthreads();
     const unsigned tn = __builtin_amdgcn_readfirstlane(tk[(it + 1) & 1]);
-    const Work3 wn = decode3<FUSED ? 2 : 0>(sc, tn);
+    const Work3 wn = decode3<0>(sc, tn);
     // the next unit's first member steps in flight during this unit's tail
     // (wave 0 after its chain wait: vmcnt counts in order, so a prefetch
     // issued before the poll would hold the poll back until it lands)
@@ -706,30 +647,20 @@ EKS_DEV unsigned k3_fwd_run(const SmoothArgs &a, const Plan3 &p, const Sched3 &s
         Elem<R> Ep;
         Ep.load(&shX[w - 1][0][l], 64);
         ok = compose_state<R>(m, P, Ep) && ok;
-        if constexpr (FUSED) state_store_pl_wt<R>(fst, f0 * KS, B, b, m, P);
-        else store_state_pl<R>(fst, f0 * KS, B, b, m, P);
+        store_state_pl<R>(fst, f0 * KS, B, b, m, P);
       }
       if constexpr (FPW > 1) {
         if (f0 + 1 < p.NCf) {
           Elem<R> Ea;
           Ea.load(&shA[w][0][l], 64);
           ok = compose_state<R>(m, P, Ea) && ok;
-          if constexpr (FUSED) state_store_pl_wt<R>(fst, (f0 + 1) * KS, B, b, m, P);
-          else store_state_pl<R>(fst, (f0 + 1) * KS, B, b, m, P);
+          store_state_pl<R>(fst, (f0 + 1) * KS, B, b, m, P);
         }
       }
     }
     if (lane_ok)
       flag(a.status, b, (ok ? 0 : EKS_STATUS_SCAN) | (okf ? 0 : EKS_STATUS_SINGULAR));
-    // FUSED: every wave's fine-start stores drained before the barrier, then
-    // one flag for the unit (the next unit's prefetch, if issued, is waited
-    // for too: vmcnt counts loads and stores in order)
-    if constexpr (FUSED) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();  // LDS free for the next unit
-    if constexpr (FUSED)
-      if (threadIdx.x == 0)
-        __hip_atomic_store((k3_gu32 *)(done + cu * p.ng + grp), 1u, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
     t = tn;
     wk = wn;
     ++it;
@@ -745,8 +676,8 @@ __global__ __launch_bounds__(64 * kWV) void k3_fwd(SmoothArgs a, Plan3 p, Sched3
   if (threadIdx.x == 0) tk[0] = atomicAdd(ctr, 1u);
   __syncthreads();
   int it = 0;
-  k3_fwd_run<R, N, E, T, AI, CI, false>(a, p, sc, __builtin_amdgcn_readfirstlane(tk[0]), lds, tk,
-                                        ctr, it);
+  k3_fwd_run<R, N, E, T, AI, CI>(a, p, sc, __builtin_amdgcn_readfirstlane(tk[0]), lds, tk, ctr,
+                                 it);
 }
 
 // ---------------------------------------------------------------------------
@@ -778,35 +709,65 @@ EKS_DEV void touch_model(Model<R, N> &md) {
       for (int k = 0; k < R; ++k) asm volatile("" : "+v"(md.C[j][k]));
 }
 
-// The k3_bwd units of consecutive tickets from t on (a run ends at the first
-// ticket that is not a k3_bwd unit, which is returned).  FUSED: each wave
-// first waits for the k3_fwd unit that stored its fine chunk's start state.
-// LB: the backward chain's look-back (publish the unit's maps, walk, fold).
+// The k3_bwd units of consecutive tickets from t on (the run ends when the
+// tickets run out).  LB: the backward chain's look-back (publish the unit's maps, walk, fold).
 // It only pays where few groups share the chip (the 8-GPU shard's k3_bwd:
 // 0.365 -> 0.348 ms) and adds SGPR pressure to the hot loop (21 -> 153
 // v_readlane in the ISA; config 4 measured the same either way), so it is a
 // separate instantiation, launched for small batches (a3_bwd_lookback).
-template <int R, int N, int E, typename T, int AI, int CI, bool NLL, bool FUSED, bool LB = true>
+template <int R, int N, int E, typename T, int AI, int CI, bool NLL, bool LB>
 EKS_DEV unsigned k3_bwd_run(const SmoothArgs &a, const Plan3 &p, const Sched3 &sc, unsigned t,
                             double *lds, unsigned *tk, unsigned *ctr, int &it) {
   constexpr int KS = R + Sym<R>::len, MP = R * R + R;
   constexpr int D = kK3D;
   constexpr int NR = reg_steps3(R, N), NL = lds_steps3(R, N), LF = NR + NL;
-  constexpr int KPUF = kWV * fwd_fpw<R>();  // fine chunks per k3_fwd unit
   auto &fs = *reinterpret_cast<double (*)[NL][KS][64 * kWV]>(lds);  // filtered states, first NL steps
   auto &shM = *reinterpret_cast<double (*)[kWV - 1][MP][64]>(lds + NL * KS * 64 * kWV);  // maps of waves 1..3
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63;
   const int tid = threadIdx.x;
   const long long B = a.B, TT = a.T;
   unsigned *flags = (unsigned *)(a.ws + p.flag2_off);
-  const unsigned *done = (const unsigned *)(a.ws + p.flag3_off);
   const double *fst = (const double *)(a.ws + p.fst_off);
   double *inc = (double *)(a.ws + p.inc2_off);
   double *agg2 = (double *)(a.ws + p.agg2_off);
   const double *prm = (const double *)(a.ws + p.prm_off);
   const bool vec2 = N == 2 && a.oj == 1 && ((a.ob | a.ot) & 1) == 0 &&
                     (((uintptr_t)a.out) & 15) == 0;
-  Work3 wk = decode3<FUSED ? 2 : 1>(sc, t);  // uniform: every index below in SGPRs
+  Work3 wk = decode3<1>(sc, t);  // uniform: every index below in SGPRs
+  // the member ring, persisting across the units of the run
+  typename SrcOf<E, N, T, D>::type src;
+  src.init(a);
+  // The head of unit wk_ for this wave: its model, the start state of its
+  // fine chunk and its first D member steps.  Issued for the next unit while
+  // this one runs its chain and backward sweep, so a unit starts with its
+  // loads landed instead of one HBM round trip of prologue.  Lanes past the
+  // last trajectory load trajectory 0 (wave-uniform branches only).
+  auto head = [&](const Work3 &wk_, Model<R, N> &md_, double (&m_)[R], double (&P_)[R][R]) {
+    if (wk_.phase != 1) return;
+    const long long f_ = (p.NCc - 1 - wk_.c) * kWV + w;
+    if (f_ >= p.NCf) return;
+    const unsigned b_ = (unsigned)(wk_.grp * 64 + l);
+    const unsigned bl_ = (long long)b_ < B ? b_ : 0u;
+    load_model_pl<R, N, AI, CI>(prm, B, bl_, f_ == 0, md_);
+    if (f_ == 0) {
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        m_[i] = md_.m0[i];
+#pragma unroll
+        for (int j = 0; j < R; ++j) P_[i][j] = md_.S0[i][j];
+      }
+    } else {
+      load_state_pl<R>(fst, f_ * KS, B, bl_, m_, P_);
+    }
+    src.lane(a, bl_);
+    const long long s_ = f_ * p.L, e_ = min(TT, s_ + p.L);
+#pragma unroll
+    for (int q = 0; q < D; ++q)
+      if (s_ + q < e_) src.fetch(q, s_ + q);
+  };
+  Model<R, N> md;        // the current unit's model
+  double m[R], P[R][R];  // its fine chunk's start state, then the running filter state
+  head(wk, md, m, P);
   while (wk.phase == 1) {
     unsigned tnext = 0;
     if (tid == 0) tnext = atomicAdd(ctr, 1u);
@@ -817,105 +778,93 @@ EKS_DEV unsigned k3_bwd_run(const SmoothArgs &a, const Plan3 &p, const Sched3 &s
     const bool lane_ok = (long long)b < B;
     const bool live = lane_ok && f < p.NCf;
     bool ok = true, okc = true;  // recursions, and the chain wait
-    Model<R, N> md;
     // the last NR steps keep their RTS gains (J_t, d_t) from the forward
     // sweep in registers; the first NL keep filtered states in LDS
     double Jr[NR][R][R], dr[NR][R];
     Affine<R> Mp;       // this chunk's RTS map: ms[s] = G ms[e] + g
     Mp.set_identity();
     const long long s = f * p.L, e = min(TT, s + p.L);
+    // a whole fine chunk with a successor step after it (wave-uniform)
+    const bool full = e - s == LF && e < TT;
     // wave-uniform branch: lanes past the last trajectory run on trajectory
     // 0's data and store nothing
     const unsigned bl = lane_ok ? b : 0u;
-    if (f < p.NCf) {
-      // FUSED: the start state of fine chunk f was stored by k3_fwd unit
-      // (f - 1) / KPUF of this group (an earlier ticket)
-      if constexpr (FUSED)
-        if (f >= 1 && !wait_flag(done + ((f - 1) / KPUF) * p.ng + grp, a.wait_ticks)) okc = false;
-      load_model_pl<R, N, AI, CI>(prm, B, bl, f == 0, md);
-      double m[R], P[R][R];
-      if (f == 0) {
-#pragma unroll
-        for (int i = 0; i < R; ++i) {
-          m[i] = md.m0[i];
-#pragma unroll
-          for (int j = 0; j < R; ++j) P[i][j] = md.S0[i][j];
-        }
-      } else if constexpr (FUSED) {
-        state_load_pl_wt<R>(fst, f * KS, B, bl, m, P);
-      } else {
-        load_state_pl<R>(fst, f * KS, B, bl, m, P);
-      }
-      typename SrcOf<E, N, T, D>::type src;
-      src.init(a);
-      src.lane(a, bl);
-#pragma unroll
-      for (int q = 0; q < D; ++q)
-        if (s + q < e) src.fetch(q, s + q);
+    if (f < p.NCf) {  // (model, start state and first steps: head())
       typename std::conditional<NLL, NllAcc, NoAcc>::type acc;  // NLL shares only when asked for
+      // one forward step i (time tt) of the re-run.  FULL: a whole chunk that
+      // is not the trajectory's last (every step present, every step has a
+      // successor): no run-time guards, so no value merges at each step
+      auto fwd_step = [&](const int i, const long long tt, auto full) {
+        constexpr bool FULL = decltype(full)::value;
+        double avg[N], rv[N], y[N];
+        src.get(i % D, avg, rv);
+        if (FULL ? i + D < LF : tt + D < e) src.fetch(i % D, tt + D);
 #pragma unroll
-      for (int i = 0; i < LF; ++i) {
-        const long long tt = s + i;
-        if (tt < e) {
-          double avg[N], rv[N], y[N];
-          src.get(i % D, avg, rv);
-          if (tt + D < e) src.fetch(i % D, tt + D);
+        for (int j = 0; j < N; ++j) y[j] = avg[j] - md.off[j];
+        if (FULL ? (i > 0 || f > 0) : tt > 0) kf_predict<R, AI>(m, P, md.A, md.Q);
+        kf_update<R, N, CI, decltype(acc)>(m, P, md.C, y, rv, acc, ok);
+        if (i < NL) {
+          double st[KS];
+          int k = 0;
 #pragma unroll
-          for (int j = 0; j < N; ++j) y[j] = avg[j] - md.off[j];
-          if (tt > 0) kf_predict<R, AI>(m, P, md.A, md.Q);
-          kf_update<R, N, CI, decltype(acc)>(m, P, md.C, y, rv, acc, ok);
-          if (i < NL) {
-            double st[KS];
-            int k = 0;
+          for (int u = 0; u < R; ++u) st[k++] = m[u];
 #pragma unroll
-            for (int u = 0; u < R; ++u) st[k++] = m[u];
+          for (int u = 0; u < R; ++u)
 #pragma unroll
-            for (int u = 0; u < R; ++u)
+            for (int v = u; v < R; ++v) st[k++] = P[u][v];
 #pragma unroll
-              for (int v = u; v < R; ++v) st[k++] = P[u][v];
-#pragma unroll
-            for (int u = 0; u < KS; ++u) fs[i < NL ? i : 0][u][tid] = st[u];
-          }
-          const int ir = i >= NL ? i - NL : 0;
-          // the chunk's map in forward order: G <- G J_t, g <- g + G d_t
-          // (the trajectory's last step: ms[T-1] = mf[T-1], a constant)
-          if (tt + 1 < TT) {
-            double J[R][R], d[R];
-            ok = rts_gain<R, AI>(m, P, md.A, md.Q, J, d) && ok;
-            if (i >= NL) {
-#pragma unroll
-              for (int u = 0; u < R; ++u) {
-                dr[ir][u] = d[u];
-#pragma unroll
-                for (int v = 0; v < R; ++v) Jr[ir][u][v] = J[u][v];
-              }
-            }
-            Affine<R> step;
-#pragma unroll
-            for (int u = 0; u < R; ++u) {
-              step.g[u] = d[u];
-#pragma unroll
-              for (int v = 0; v < R; ++v) step.G[u][v] = J[u][v];
-            }
-            Mp = Mp.after(step);
-          } else {
-            if (i >= NL) {
-#pragma unroll
-              for (int u = 0; u < R; ++u) dr[ir][u] = m[u];
-            }
-#pragma unroll
-            for (int u = 0; u < R; ++u) {
-              double sg = Mp.g[u];
-#pragma unroll
-              for (int v = 0; v < R; ++v) sg = fma(Mp.G[u][v], m[v], sg);
-              Mp.g[u] = sg;
-            }
-#pragma unroll
-            for (int u = 0; u < R; ++u)
-#pragma unroll
-              for (int v = 0; v < R; ++v) Mp.G[u][v] = 0.0;
-          }
+          for (int u = 0; u < KS; ++u) fs[i < NL ? i : 0][u][tid] = st[u];
         }
+        const int ir = i >= NL ? i - NL : 0;
+        // the chunk's map in forward order: G <- G J_t, g <- g + G d_t
+        // (the trajectory's last step: ms[T-1] = mf[T-1], a constant)
+        if (FULL || tt + 1 < TT) {
+          double J[R][R], d[R];
+          ok = rts_gain<R, AI>(m, P, md.A, md.Q, J, d) && ok;
+          if (i >= NL) {
+#pragma unroll
+            for (int u = 0; u < R; ++u) {
+              dr[ir][u] = d[u];
+#pragma unroll
+              for (int v = 0; v < R; ++v) Jr[ir][u][v] = J[u][v];
+            }
+          }
+          Affine<R> step;
+#pragma unroll
+          for (int u = 0; u < R; ++u) {
+            step.g[u] = d[u];
+#pragma unroll
+            for (int v = 0; v < R; ++v) step.G[u][v] = J[u][v];
+          }
+          Mp = Mp.after(step);
+        } else {
+          if (i >= NL) {
+#pragma unroll
+            for (int u = 0; u < R; ++u) dr[ir][u] = m[u];
+          }
+#pragma unroll
+          for (int u = 0; u < R; ++u) {
+            double sg = Mp.g[u];
+#pragma unroll
+            for (int v = 0; v < R; ++v) sg = fma(Mp.G[u][v], m[v], sg);
+            Mp.g[u] = sg;
+          }
+#pragma unroll
+          for (int u = 0; u < R; ++u)
+#pragma unroll
+            for (int v = 0; v < R; ++v) Mp.G[u][v] = 0.0;
+        }
+      };
+      if (full) {
+#pragma unroll
+        for (int i = 0; i < LF; ++i) {
+          fwd_step(i, s + i, std::true_type{});
+          __builtin_amdgcn_sched_barrier(0);  // one step's registers at a time
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < LF; ++i)
+          if (s + i < e) fwd_step(i, s + i, std::false_type{});
       }
       if (NLL && lane_ok) pl((double *)(a.ws + p.nllp_off), f, B, b) = acc.value((double)(e - s) * N);
       // the model registers the backward sweep reads (offsets; Q, A, C when
@@ -938,7 +887,17 @@ EKS_DEV unsigned k3_bwd_run(const SmoothArgs &a, const Plan3 &p, const Sched3 &s
 #pragma unroll
       for (int u = 0; u < R; ++u) shM[w - 1][k++][l] = Mp.g[u];
     }
+    if (tid == 0) tk[(it + 1) & 1] = tnext;
     __syncthreads();
+    // the next unit (its ticket taken at this unit's start): its head is
+    // loaded during this unit's chain and backward sweep -- waves 1-3 now,
+    // wave 0 after its chain wait (vmcnt counts in order: a prefetch issued
+    // before the poll would hold the poll back until it lands)
+    const unsigned tn = __builtin_amdgcn_readfirstlane(tk[(it + 1) & 1]);
+    const Work3 wn = decode3<1>(sc, tn);
+    Model<R, N> mdn;
+    double mn[R], Pn[R][R];
+    if (w != 0) head(wn, mdn, mn, Pn);
     double ms[R];  // smoothed mean at the first step after this chunk
     if (w == 0) {
       // the chain: the mean at the first step of coarse chunk cc+1, published
@@ -1021,6 +980,7 @@ EKS_DEV unsigned k3_bwd_run(const SmoothArgs &a, const Plan3 &p, const Sched3 &s
           for (int u = 0; u < R; ++u) st_wt(&pl(inc, cc * R + u, B, b), x[u]);
         publish_flag(flags + grp * p.NCc + cc, l, kIncReady);
       }
+      head(wn, mdn, mn, Pn);
     }
     __syncthreads();
     if (w >= 1)
@@ -1085,81 +1045,73 @@ EKS_DEV unsigned k3_bwd_run(const SmoothArgs &a, const Plan3 &p, const Sched3 &s
         for (int i = 0; i < R; ++i) ms[i] = nx[i];
       };
       // the last NR steps from registers, then the first NL from LDS
+      auto bwd_reg = [&](const int i, const long long tt, auto fullc) {
+        double nx[R];
 #pragma unroll
-      for (int i = LF - 1; i >= NL; --i) {
-        const long long tt = s + i;
-        if (tt < e) {
-          double nx[R];
+        for (int u = 0; u < R; ++u) {
+          double sm = dr[i - NL][u];
 #pragma unroll
-          for (int u = 0; u < R; ++u) {
-            double sm = dr[i - NL][u];
+          for (int v = 0; v < R; ++v) sm = fma(Jr[i - NL][u][v], ms[v], sm);
+          nx[u] = sm;
+        }
+        if constexpr (decltype(fullc)::value) {
 #pragma unroll
-            for (int v = 0; v < R; ++v) sm = fma(Jr[i - NL][u][v], ms[v], sm);
-            nx[u] = sm;
-          }
+          for (int u = 0; u < R; ++u) ms[u] = nx[u];
+        } else {
           const bool last = tt + 1 == TT;  // ms[T-1] = mf[T-1] (J_t unset)
 #pragma unroll
           for (int u = 0; u < R; ++u) ms[u] = last ? dr[i - NL][u] : nx[u];
-          emit(tt);
         }
-      }
+        emit(tt);
+      };
+      auto bwd_lds = [&](const int i, const long long tt) {
+        double st[KS];
 #pragma unroll
-      for (int i = NL - 1; i >= 0; --i) {
-        const long long tt = s + i;
-        if (tt < e) {
-          double st[KS];
+        for (int u = 0; u < KS; ++u) st[u] = fs[i][u][tid];
+        rts_step(st, tt);
+        emit(tt);
+      };
+      if (full) {
 #pragma unroll
-          for (int u = 0; u < KS; ++u) st[u] = fs[i][u][tid];
-          rts_step(st, tt);
-          emit(tt);
-        }
+        for (int i = LF - 1; i >= NL; --i) bwd_reg(i, s + i, std::true_type{});
+#pragma unroll
+        for (int i = NL - 1; i >= 0; --i) bwd_lds(i, s + i);
+      } else {
+#pragma unroll
+        for (int i = LF - 1; i >= NL; --i)
+          if (s + i < e) bwd_reg(i, s + i, std::false_type{});
+#pragma unroll
+        for (int i = NL - 1; i >= 0; --i)
+          if (s + i < e) bwd_lds(i, s + i);
       }
     }
     if (lane_ok)
       flag(a.status, b, (ok ? 0 : EKS_STATUS_SINGULAR) | (okc ? 0 : EKS_STATUS_SCAN));
-    if (tid == 0) tk[(it + 1) & 1] = tnext;
-    __syncthreads();  // LDS free for the next unit, its ticket visible
-    t = __builtin_amdgcn_readfirstlane(tk[(it + 1) & 1]);
-    wk = decode3<FUSED ? 2 : 1>(sc, t);
+    __syncthreads();  // LDS free for the next unit
+    md = mdn;
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      m[i] = mn[i];
+#pragma unroll
+      for (int j = 0; j < R; ++j) P[i][j] = Pn[i][j];
+    }
+    t = tn;
+    wk = wn;
     ++it;
   }
   return t;
 }
 
 template <int R, int N, int E, typename T, int AI, int CI, bool NLL, bool LB>
-__global__ __launch_bounds__(64 * kWV) void k3_bwd(SmoothArgs a, Plan3 p, Sched3 sc) {
+__global__ __launch_bounds__(64 * kWV, 2) void k3_bwd(SmoothArgs a, Plan3 p, Sched3 sc) {
   __shared__ double lds[bwd_lds_doubles<R, N>()];
   __shared__ unsigned tk[2];
   unsigned *ctr = (unsigned *)a.ws + 32;
   if (threadIdx.x == 0) tk[0] = atomicAdd(ctr, 1u);
   __syncthreads();
   int it = 0;
-  k3_bwd_run<R, N, E, T, AI, CI, NLL, false, LB>(a, p, sc, __builtin_amdgcn_readfirstlane(tk[0]), lds,
-                                             tk, ctr, it);
-}
-
-// Both passes in one persistent launch (schedule: Sched3 mode 2): runs of
-// k3_fwd units and runs of k3_bwd units as the tickets come.
-template <int R, int N, int E, typename T, int AI, int CI, bool NLL, bool FWD_NT>
-__global__ __launch_bounds__(64 * kWV) void k3_fused(SmoothArgs a, Plan3 p, Sched3 sc) {
-  constexpr int LD = fwd_lds_doubles<R>() > bwd_lds_doubles<R, N>() ? fwd_lds_doubles<R>()
-                                                                    : bwd_lds_doubles<R, N>();
-  __shared__ double lds[LD];
-  __shared__ unsigned tk[2];
-  unsigned *ctr = (unsigned *)a.ws;
-  if (threadIdx.x == 0) tk[0] = atomicAdd(ctr, 1u);
-  __syncthreads();
-  unsigned t = __builtin_amdgcn_readfirstlane(tk[0]);
-  int it = 0;
-  while (true) {
-    const Work3 wk = decode3<2>(sc, t);
-    if (wk.phase == 0)
-      t = k3_fwd_run<R, N, E, T, AI, CI, true, FWD_NT>(a, p, sc, t, lds, tk, ctr, it);
-    else if (wk.phase == 1)
-      t = k3_bwd_run<R, N, E, T, AI, CI, NLL, true>(a, p, sc, t, lds, tk, ctr, it);
-    else
-      break;
-  }
+  k3_bwd_run<R, N, E, T, AI, CI, NLL, LB>(a, p, sc, __builtin_amdgcn_readfirstlane(tk[0]), lds, tk,
+                                         ctr, it);
 }
 
 // NLL of each trajectory = sum of its fine chunks' shares (fixed order)
@@ -1174,17 +1126,6 @@ __global__ __launch_bounds__(64) void k3_nll(SmoothArgs a, Plan3 p) {
 #pragma unroll
   for (int k = 32; k >= 1; k >>= 1) s += __shfl_xor(s, k, 64);
   if (l == 0) a.nll[b] = s;
-}
-
-// One launch for both passes or two (eks_debug_set(EKS_DBG_A3_MODE): 1 = two
-// launches, 2 = one launch, all forward units first; 0 = the default, two
-// launches: measured equal at config 4 and its 8-GPU shard).
-// Returns the batch size in groups of the one-launch schedule, 0 for two
-// launches.  (The batched schedule, small GB, was measured 5-15x slower: with
-// one or a few groups per batch the chains of a batch run nearly alone on
-// the chip; it is kept in decode3 but not launched.)
-inline long long a3_fused_groups(const Plan3 &p) {
-  return g_a3_mode >= 2 ? p.ng : 0;
 }
 
 // k3_bwd's look-back instantiation (LB): for batches of at most kLbGroups
@@ -1217,36 +1158,20 @@ int launch_algo3_one(const SmoothArgs &a) {
     hipLaunchKernelGGL((k_model_planes<R, N, AI, CI>), dim3(grid_for(a.B, 256)), dim3(256), 0, a.stream,
                        a.params, a.B, (double *)(a.ws + p.prm_off), a.status);
     if ((rc = check_launch("k_model_planes"))) return rc;
-    // (the one-launch form is compiled for the single-view model only: the
-    // throughput shape; others keep two launches)
-    constexpr bool kCanFuse = R == 2 && N == 2 && AI == kAId && CI == kCId;
-    const long long gb = kCanFuse ? a3_fused_groups(p) : 0;
-    if constexpr (kCanFuse) if (gb > 0) {  // both passes in one launch
-      prof_mark(a.stream, "k3_fused");
-      const Sched3 sc = make_sched3(p, 2, gb);
-      const long long units = p.units_f + p.units;
-      if (a.nll)
-        hipLaunchKernelGGL((k3_fused<R, N, EE, Tp, AI, CI, true, true>),
-                           dim3(persistent_grid<k3_fused<R, N, EE, Tp, AI, CI, true, true>>(units)),
-                           dim3(64 * kWV), 0, a.stream, a, p, sc);
-      else
-        hipLaunchKernelGGL((k3_fused<R, N, EE, Tp, AI, CI, false, true>),
-                           dim3(persistent_grid<k3_fused<R, N, EE, Tp, AI, CI, false, true>>(units)),
-                           dim3(64 * kWV), 0, a.stream, a, p, sc);
-      if ((rc = check_launch("k3_fused"))) return rc;
-    }
-    if (!kCanFuse || gb <= 0) {
+    // the single-view model: the throughput shape (config 4)
+    constexpr bool kSingleView = R == 2 && N == 2 && AI == kAId && CI == kCId;
+    {
       prof_mark(a.stream, "k3_fwd");
       hipLaunchKernelGGL((k3_fwd<R, N, EE, Tp, AI, CI>),
                          dim3(persistent_grid<k3_fwd<R, N, EE, Tp, AI, CI>>(p.units_f)),
-                         dim3(64 * kWV), 0, a.stream, a, p, make_sched3(p, 0, 0));
+                         dim3(64 * kWV), 0, a.stream, a, p, make_sched3(p, 0));
       if ((rc = check_launch("k3_fwd"))) return rc;
       prof_mark(a.stream, "k3_bwd");
-      const Sched3 sb = make_sched3(p, 1, 0);
+      const Sched3 sb = make_sched3(p, 1);
       // the look-back instantiation only for small batches of the
-      // single-view shape (kCanFuse: the throughput shape)
+      // single-view shape
       bool lb = false;
-      if constexpr (kCanFuse) lb = a3_bwd_lookback(p);
+      if constexpr (kSingleView) lb = a3_bwd_lookback(p);
       if (a.nll) {
         if (lb)
           hipLaunchKernelGGL((k3_bwd<R, N, EE, Tp, AI, CI, true, true>),

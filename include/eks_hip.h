@@ -328,10 +328,9 @@ int eks_interp1d(const double *x, int64_t nx, const double *y, int64_t ncol, int
  *                          one block per row, 2 = split (both must give the
  *                          same threshold and kept-frame mask).  The
  *                          workspace size follows the setting.
- *   EKS_DBG_A3_MODE        algo 3's launch form: 0 = the default (two
- *                          launches), 1 = two launches (forward pass,
- *                          backward pass), 2 = one persistent launch, all
- *                          forward units first.  Results are bit-identical.
+ *   EKS_DBG_A3_MODE        retired (round 5): algo 3 has one launch form,
+ *                          the forward pass then the backward pass; the key
+ *                          still round-trips its value and changes nothing.
  *   EKS_DBG_A3_LB          algo 3's backward look-back: 0 = automatic (batches
  *                          of at most 48 64-trajectory groups), 1 = never,
  *                          2 = always.  Results are bit-identical.

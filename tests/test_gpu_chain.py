@@ -142,29 +142,28 @@ def test_algo3_shard_size_lookback_bit_identical(torch):
 
 
 @pytest.mark.parametrize("B,T", [(700, 3000), (64, 1000), (2176, 2000)])
-def test_algo3_launch_forms_bit_identical(torch, B, T):
-    """algo 3 as two launches and as one persistent launch with all forward
-    units first: the same operations in the same association order, so the
-    same bits (outputs, smoothed means, NLL); and the forced time-out flags
-    every trajectory in the one-launch form."""
+def test_algo3_lookback_forms_bit_identical(torch, B, T):
+    """k3_bwd with and without its decoupled look-back (EKS_DBG_A3_LB 1 / 2):
+    the same operations in the same association order, so the same bits
+    (outputs, smoothed means, NLL); and the forced time-out flags every
+    trajectory in both forms.  (Round 4's one-launch form of both passes was
+    removed in round 5: it measured no better at any size.)"""
     from eks_amd import _lib, batch
     d, params, flags = _singleview(torch, B, T, 900 + B)
     runs = {}
-    prev = _lib.debug_set(_lib.EKS_DBG_A3_MODE, 1)
+    prev = _lib.debug_set(_lib.EKS_DBG_A3_LB, 1)
     try:
-        for mode in (1, 2):
-            _lib.debug_set(_lib.EKS_DBG_A3_MODE, mode)
-            runs[mode] = batch.smooth(d, params, n=2, r=2, algo=3, flags=flags, want_ms=True,
-                                      want_nll=True)
-            assert (runs[mode]["status"] == 0).all(), mode
-        _lib.debug_set(_lib.EKS_DBG_A3_MODE, 2)
-        with _Forced():
-            bad = batch.smooth(d, params, n=2, r=2, algo=3, flags=flags)
-            torch.cuda.synchronize()
-            if T > 256:  # (more than one unit per trajectory: every unit but the first waits)
-                assert (bad["status"].cpu().numpy() & _lib.EKS_STATUS_SCAN).all()
+        for lb in (1, 2):
+            _lib.debug_set(_lib.EKS_DBG_A3_LB, lb)
+            runs[lb] = batch.smooth(d, params, n=2, r=2, algo=3, flags=flags, want_ms=True,
+                                    want_nll=True)
+            assert (runs[lb]["status"] == 0).all(), lb
+            with _Forced():
+                bad = batch.smooth(d, params, n=2, r=2, algo=3, flags=flags)
+                torch.cuda.synchronize()
+                if T > 256:  # (more than one unit per trajectory: every unit but the first waits)
+                    assert (bad["status"].cpu().numpy() & _lib.EKS_STATUS_SCAN).all()
     finally:
-        _lib.debug_set(_lib.EKS_DBG_A3_MODE, prev)
-    for mode in (2,):
-        for k in ("out", "ms", "nll"):
-            assert torch.equal(runs[mode][k], runs[1][k]), (mode, k)
+        _lib.debug_set(_lib.EKS_DBG_A3_LB, prev)
+    for k in ("out", "ms", "nll"):
+        assert torch.equal(runs[2][k], runs[1][k]), k

@@ -817,6 +817,45 @@ def test_torch_ops_forward_backward_match_core(torch):
         np.testing.assert_array_equal(CV[0].cpu().numpy(), CV_r)
 
 
+def test_torch_ops_host_model_tensors_and_shapes(torch):
+    """Model tensors on the host (numpy-derived) are moved to the call's device
+    by eks::forward / backward / newton_filter -- same bits as device tensors
+    (the Python shims they replace moved them too) -- and model arrays of the
+    wrong shape are a RuntimeError before any kernel runs, never an
+    out-of-bounds device read (round-4 advisor findings)."""
+    import eks_amd.ops  # noqa: F401
+    g = np.load(CORE[1])
+    h = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.float64))  # noqa: E731
+    d = lambda a: h(a).cuda()  # noqa: E731
+    y, ev = d(g["y"])[None], d(g["ev"])[None]
+    ref = torch.ops.eks.forward(y, ev, d(g["m0"]), d(g["S0"]), d(g["A"]), d(g["Q"]), d(g["C"]))
+    got = torch.ops.eks.forward(y, h(g["ev"])[None], h(g["m0"]), h(g["S0"]), h(g["A"]), h(g["Q"]),
+                                h(g["C"]))
+    for x0, x1 in zip(ref, got):
+        assert torch.equal(x0, x1)
+    mf, Vf, S = ref[:3]
+    b0 = torch.ops.eks.backward(mf, Vf, S, d(g["A"]))
+    b1 = torch.ops.eks.backward(mf, Vf.cpu(), S.cpu(), h(g["A"]))
+    for x0, x1 in zip(b0, b1):
+        assert torch.equal(x0, x1)
+    r, n = g["m0"].shape[-1], g["y"].shape[-1]
+    E = np.eye(r)
+    q0 = torch.ops.eks.newton_filter(y, ev, d(g["m0"]), d(g["S0"]), d(g["A"]), d(g["C"]), d(E), 1)
+    q1 = torch.ops.eks.newton_filter(y, ev, h(g["m0"]), h(g["S0"]), h(g["A"]), h(g["C"]), h(E), 1)
+    assert torch.equal(q0[0], q1[0]) and torch.equal(q0[1], q1[1])
+    bad = d(np.zeros((r + 1, r + 1)))
+    with pytest.raises(RuntimeError, match="shape"):
+        torch.ops.eks.forward(y, ev, d(g["m0"]), d(g["S0"]), bad, d(g["Q"]), d(g["C"]))
+    with pytest.raises(RuntimeError, match="shape"):
+        torch.ops.eks.forward(y, ev, d(g["m0"])[None].repeat(2, 1), d(g["S0"]), d(g["A"]),
+                              d(g["Q"]), d(g["C"]))
+    with pytest.raises(RuntimeError, match="shape"):
+        torch.ops.eks.backward(mf, Vf[:, :-1], S, d(g["A"]))
+    with pytest.raises(RuntimeError, match="shape"):
+        torch.ops.eks.newton_filter(y, ev, d(g["m0"]), d(g["S0"]), d(g["A"]), d(np.zeros((n + 1, r))),
+                                    d(E), 1)
+
+
 # -------------------------------------------------------------------------
 # fit -> smooth ensemble hand-off (EKS_YEV32 / EKS_YEV64): bit-identical
 @pytest.mark.parametrize("kind,V,E,dtype,mode,algo", [
