@@ -40,6 +40,7 @@
 
 #include <cmath>
 #include <cstdint>
+#include <utility>
 
 #include "../../include/eks_hip.h"
 #include "eks_common.hpp"
@@ -119,6 +120,30 @@ struct ZeroSpan {
 
 constexpr int kTile = 16;  // frames per register tile: one 128-byte row segment per lane
 
+// the same from E x N member values already in registers (raw[j][e])
+template <int E, int N, typename T>
+EKS_DEV void frame_ensemble_raw(const T (&raw)[N][E], bool median, double (&y)[N],
+                                double (&ev)[N], double &v) {
+  v = -1.0;
+  bool nan = false;
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    double avg, var;
+    ensemble_reduce<E, T>(raw[j], median, avg, var);
+    y[j] = avg;
+    ev[j] = var;
+    nan |= (var != var);
+    v = var > v ? var : v;
+  }
+  if (nan) v = __builtin_nan("");
+}
+
+// frames of member loads in flight per lane in k_fit_worst (compiled E: a
+// register ring; 4 x 10 loads at E = 5, n = 2.  Round 4's form loaded one
+// column of E members and waited for it: 5 loads in flight per wave, 4.2 TB/s)
+constexpr int kWorstD = 4;
+static_assert(16 % kWorstD == 0, "the ring slots repeat every register tile");
+
 template <int E, int N, typename T, typename YT>
 __global__ __launch_bounds__(256) void k_fit_worst(const T *__restrict__ obs, FitShape sh,
                                                    long long sb, long long st, long long se,
@@ -142,23 +167,54 @@ __global__ __launch_bounds__(256) void k_fit_worst(const T *__restrict__ obs, Fi
   }
   const T *pb = obs + b * sb;
   const long long ntiles = sh.Lc / kTile;  // Lc is a multiple of kTile
+  // one frame's outputs: the y / ev hand-off planes, the trajectory's shift K
+  auto frame_out = [&](long long u, const double (&y)[N], const double (&ev)[N]) {
+    if (u == 0)  // the trajectory's shift for the accumulation (frame 0's ensemble)
+#pragma unroll
+      for (int j = 0; j < N; ++j) ks.K[b * N + j] = y[j];
+    if (yo.y)
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        ((YT *)yo.y)[(u * N + j) * sh.B + b] = (YT)y[j];
+        yo.ev[(u * N + j) * sh.B + b] = ev[j];
+      }
+  };
+  // compiled E: the lane's frames stream through a ring kWorstD frames deep
+  // (reads past the lane's last frame are clamped to it: cache hits)
+  constexpr int RE = E > 0 ? E : 1;
+  T ring[kWorstD][N][RE];
+  auto fetch = [&](int slot, long long u) {
+    u = u < t1 ? u : t1 - 1;
+    const T *p = pb + u * st;
+#pragma unroll
+    for (int j = 0; j < N; ++j)
+#pragma unroll
+      for (int e = 0; e < RE; ++e) ring[slot][j][e] = p[j * sj + e * se];
+  };
+  if constexpr (E > 0)
+    if (active && t1 > t0)
+#pragma unroll
+      for (int q = 0; q < kWorstD; ++q) fetch(q, t0 + q);
   for (long long kt = 0; kt < ntiles; ++kt) {
     const long long t = t0 + kt * kTile;
     if (active && t + kTile <= t1) {
 #pragma unroll
       for (int k = 0; k < kTile; ++k) {
         double y[N], ev[N];
-        frame_ensemble<E, N, T>(pb + (t + k) * st, se, sj, Ert, median != 0, y, ev,
-                                tile[threadIdx.x][k]);
-        if (t + k == 0)  // the trajectory's shift for the accumulation (frame 0's ensemble)
+        if constexpr (E > 0) {
+          const int slot = k % kWorstD;
+          T raw[N][RE];
 #pragma unroll
-          for (int j = 0; j < N; ++j) ks.K[b * N + j] = y[j];
-        if (yo.y)
+          for (int j = 0; j < N; ++j)
 #pragma unroll
-          for (int j = 0; j < N; ++j) {
-            ((YT *)yo.y)[((t + k) * N + j) * sh.B + b] = (YT)y[j];
-            yo.ev[((t + k) * N + j) * sh.B + b] = ev[j];
-          }
+            for (int e = 0; e < RE; ++e) raw[j][e] = ring[slot][j][e];
+          fetch(slot, t + k + kWorstD);
+          frame_ensemble_raw<RE, N, T>(raw, median != 0, y, ev, tile[threadIdx.x][k]);
+        } else {
+          frame_ensemble<E, N, T>(pb + (t + k) * st, se, sj, Ert, median != 0, y, ev,
+                                  tile[threadIdx.x][k]);
+        }
+        frame_out(t + k, y, ev);
       }
       base[threadIdx.x] = b * sh.T + t;
     } else {
@@ -168,15 +224,7 @@ __global__ __launch_bounds__(256) void k_fit_worst(const T *__restrict__ obs, Fi
           double y[N], ev[N], v;
           frame_ensemble<E, N, T>(pb + u * st, se, sj, Ert, median != 0, y, ev, v);
           worst[b * sh.T + u] = v;
-          if (u == 0)
-#pragma unroll
-            for (int j = 0; j < N; ++j) ks.K[b * N + j] = y[j];
-          if (yo.y)
-#pragma unroll
-            for (int j = 0; j < N; ++j) {
-              ((YT *)yo.y)[(u * N + j) * sh.B + b] = (YT)y[j];
-              yo.ev[(u * N + j) * sh.B + b] = ev[j];
-            }
+          frame_out(u, y, ev);
         }
     }
     __syncthreads();
@@ -934,13 +982,55 @@ __global__ __launch_bounds__(256) void k_fit_accum(const T *__restrict__ obs, Fi
     }
     cnt += 1.0;
   };
-  if constexpr (FROM_YEV) {
-    // the ensemble of every frame is already in the y plane, and whether it
-    // is kept in k_fit_select's frame mask (8 of the 24 B per frame that
-    // reading the ev plane took).  The kept frames are taken from the mask
-    // words KB at a time with their y loads in flight together (a loop over
-    // every frame with a branch per frame had one load round trip per kept
-    // frame); frame order is kept, so the sums are those of the member path.
+  if constexpr (FROM_YEV && !WAVE_MERGE) {
+    // Trajectory-fastest lanes: the wave's 64 trajectories read the SAME
+    // frame at each step, so every frame's y is one coalesced row segment;
+    // the y plane streams through a ring kAccD frames deep and the kept bit
+    // of k_fit_select's mask decides which frames are summed.  (Round 4
+    // gathered only the kept frames, four at a time: each lane a different
+    // frame, so every 4-byte load was its own 64-byte request -- 1.79 GB
+    // fetched for the 0.35 GB kept, 3.8 TB/s.)  Frame order is kept: the
+    // sums are those of the member path.
+    constexpr int kAccD = 8;
+    YT ring[kAccD][N];
+    const YT *yb = (const YT *)yi.y;
+    auto fetch = [&](int q, long long t) {
+      t = t < t1 ? t : t1 - 1;
+#pragma unroll
+      for (int j = 0; j < N; ++j) ring[q][j] = yb[(t * N + j) * sh.B + b];
+    };
+    if (t1 > t0)
+#pragma unroll
+      for (int q = 0; q < kAccD; ++q) fetch(q, t0 + q);
+    // the mask word of the current 64 frames, and the next one loaded a word
+    // ahead (vmcnt counts in order: a word loaded just before its use would
+    // drain the ring's loads issued before it)
+    const long long w0 = t0 >> 6;
+    uint64_t m = t1 > t0 ? krow[w0] : 0ull;
+    uint64_t mn = w0 + 1 < W ? krow[w0 + 1] : 0ull;
+    for (long long tb = t0; tb < t1; tb += kAccD) {
+#pragma unroll
+      for (int q = 0; q < kAccD; ++q) {
+        const long long t = tb + q;
+        if (t < t1) {
+          if (t > t0 && (t & 63) == 0) {
+            m = mn;
+            mn = (t >> 6) + 1 < W ? krow[(t >> 6) + 1] : 0ull;
+          }
+          double y[N];
+#pragma unroll
+          for (int j = 0; j < N; ++j) y[j] = (double)ring[q][j];
+          fetch(q, t + kAccD);
+          if ((m >> (t & 63)) & 1ull) take(y);
+        }
+      }
+    }
+  } else if constexpr (FROM_YEV) {
+    // WAVE_MERGE (few long trajectories, a wave = 64 chunks of one
+    // trajectory): the kept frames are taken from the mask words KB at a
+    // time with their y loads in flight together (a loop over every frame
+    // with a branch per frame had one load round trip per kept frame);
+    // frame order is kept, so the sums are those of the member path.
     constexpr int KB = 4;
     for (long long wb = t0 & ~63LL; wb < t1; wb += 64) {
       uint64_t m = krow[wb >> 6];
@@ -1257,6 +1347,27 @@ __global__ __launch_bounds__(64) void k_fit_final(long long B, const double *__r
 // ---------------------------------------------------------------------------
 constexpr int kNW = 16;
 
+// Broadcast of lane J of each 16-lane DPP row to the whole row: the groups
+// of kNW = 16 lanes are exactly the wave's DPP rows, so one v_mov_b64_dpp
+// row_newbcast:J (gfx950's 64-bit DPP broadcast) replaces a __shfl (two
+// ds_bpermute_b32 through the LDS crossbar plus their waits).  The row is
+// active or idle as a whole (the kept decision is uniform over a group).
+template <int J>
+EKS_DEV double row_bcast(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)  // (the host pass only parses device code)
+  const long v = __builtin_bit_cast(long, x);
+  const long r = __builtin_amdgcn_update_dpp(0L, v, 0x150 + J, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, r);
+#else
+  return x;
+#endif
+}
+// acc[j] += x * (x of column j) for the group's kNW columns
+template <int... J>
+EKS_DEV void row_outer(double x, double (&acc)[kNW], std::integer_sequence<int, J...>) {
+  ((acc[J] = fma(x, row_bcast<J>(x), acc[J])), ...);
+}
+
 // k_fit_worst's lanes and tiles (trajectory-fastest lanes over chunks of
 // frames: the hand-off planes' rows, B values each, are written by
 // consecutive lanes; the worst rows leave through an LDS tile) with the
@@ -1356,7 +1467,7 @@ __global__ __launch_bounds__(256) void k_fitw_accum(const T *__restrict__ obs, F
   const long long gl = blockIdx.x * (long long)blockDim.x + threadIdx.x;
   const long long pc = gl / kNW;  // (chunk, trajectory) pair: c * B + b
   if (pc >= sh.B * sh.NC) return;  // whole groups (B NC kNW lanes)
-  const int i = (int)(gl % kNW), base = (int)(threadIdx.x & 63) & ~(kNW - 1);
+  const int i = (int)(gl % kNW);  // column; the group is the lane's DPP row
   const bool own = i < n;
   const int ic = own ? i : n - 1;  // idle lanes shadow the last column (never stored)
   const long long b = pc % sh.B, c = pc / sh.B;
@@ -1376,15 +1487,13 @@ __global__ __launch_bounds__(256) void k_fitw_accum(const T *__restrict__ obs, F
     } else {
       const double d = y - last;
       D1 += d;
-#pragma unroll
-      for (int j = 0; j < kNW; ++j) D2[j] = fma(d, __shfl(d, base + j, 64), D2[j]);
+      row_outer(d, D2, std::make_integer_sequence<int, kNW>{});
       npair += 1.0;
     }
     const double z = y - K;
     last = y;
     S1 += z;
-#pragma unroll
-    for (int j = 0; j < kNW; ++j) S2[j] = fma(z, __shfl(z, base + j, 64), S2[j]);
+    row_outer(z, S2, std::make_integer_sequence<int, kNW>{});
     cnt += 1.0;
   };
   // a frame is kept when v = max over the group's columns <= th (uniform over

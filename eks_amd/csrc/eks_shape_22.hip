@@ -12,3 +12,10 @@ int launch_22(const SmoothArgs &a, int algo, long long L) {
 }
 
 }  // namespace eks
+
+#if EKS_STAMPS
+// profiling builds only (-DEKS_STAMPS=1): copy algo 3's phase stamps to the host
+extern "C" int eks_dbg_stamps(void *dst, size_t bytes) {
+  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(eks::g_stamps), bytes);
+}
+#endif

@@ -1,6 +1,6 @@
 // Compile-time tuning constants of the kernels: the measured choices, one
-// place.  (No macro overrides: variant builds for tuning experiments live in
-// tools/, e.g. tools/build_variant.sh on an edited copy of this file.)
+// place.  A few knobs take a -D override for A/B variant builds
+// (tools/build_cur.sh NAME -DKNOB=v unit.hip); the defaults are what ships.
 #pragma once
 
 namespace eks {
@@ -24,8 +24,19 @@ constexpr bool kNtOut = true;
 #endif
 constexpr bool kHandoffFences = EKS_HANDOFF_FENCES != 0;
 
-// member prefetch distance (steps) of both algo-3 passes
+// member prefetch distance (steps) of both algo-3 passes (k3_bwd: its own,
+// A/B-able with -DEKS_K3B_D=...)
 constexpr int kK3D = 2;
+#ifndef EKS_K3B_D
+#define EKS_K3B_D 2
+#endif
+constexpr int kK3BD = EKS_K3B_D;
+// k3_bwd's whole-chunk loop: a scheduling barrier after every step (one
+// step's registers live at a time); A/B with -DEKS_K3B_SCHED=0
+#ifndef EKS_K3B_SCHED
+#define EKS_K3B_SCHED 1
+#endif
+constexpr bool kK3BSched = EKS_K3B_SCHED != 0;
 
 // few-trajectory prefetch distances of algo 2's K1 / K3 (config 2: 2 / 4 / 8
 // steps all within 2 %, tools/c2_dsweep.sh -- these lanes are bound by the

@@ -59,6 +59,30 @@
 
 constexpr int kWV = 4;  // waves per unit = fine chunks per coarse chunk
 
+// In-kernel phase stamps (profiling builds only: -DEKS_STAMPS=1, read back by
+// eks_dbg_stamps / tools/stamps_run.py): s_memtime at the phase boundaries of
+// every unit, per (pass, block, unit, wave); slot 0 = the unit's (group, chunk).
+// Stored by lane 0 with a vector store.  Compiled out of the shipped library.
+#ifndef EKS_STAMPS
+#define EKS_STAMPS 0
+#endif
+constexpr int kStampBlocks = 512, kStampIts = 128;
+#if EKS_STAMPS
+static __device__ unsigned long long g_stamps[2 * kStampBlocks * kStampIts * 32];
+#define EKS_STAMP(PASS, K)                                                                    \
+  do {                                                                                        \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();                               \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < kStampBlocks && it < kStampIts)               \
+      g_stamps[(((size_t)(PASS) * kStampBlocks + blockIdx.x) * kStampIts + it) * 32 +        \
+               (threadIdx.x >> 6) * 8 + (K)] =                                               \
+          (K) == 0 ? (((unsigned long long)wk.grp << 32) | (unsigned long long)wk.c) : t_;    \
+  } while (0)
+#else
+#define EKS_STAMP(PASS, K) \
+  do {                     \
+  } while (0)
+#endif
+
 // fine chunk geometry of k3_bwd: NR steps' filtered states in registers, NL
 // in LDS; LDS per block <= 80 KB so two 256-thread blocks share a CU (the
 // register file allows two waves per SIMD), after the 3 waves' RTS maps
@@ -77,7 +101,7 @@ struct Plan3 {
   // then one flag word per unit for each pass
   size_t sync_bytes = 0, flag1_off = 0, flag2_off = 0;
   size_t fst_off = 0, inc2_off = 0, nllp_off = 0, prm_off = 0, total = 0;
-  // look-back aggregates: k3_fwd's unit elements, k3_bwd's 4 chunk maps per unit
+  // look-back aggregates: k3_fwd's unit elements, k3_bwd's unit maps
   size_t agg1_off = 0, agg2_off = 0;
 };
 
@@ -110,9 +134,10 @@ inline Plan3 make_plan3(long long B, long long T, int r, int n) {
   p.prm_off = take((size_t)param_len(n, r) * Bz * 8);  // k_model_planes
   // a unit's aggregate, published for the look-back of later units when the
   // value it waits for is not there yet: k3_fwd's element of unit c (planes
-  // c * EL ..), k3_bwd's 4 RTS maps of unit c (planes (c * kWV + v) * MP ..)
+  // c * EL ..), k3_bwd's RTS map of unit c (its 4 chunk maps composed; planes
+  // c * MP ..)
   p.agg1_off = take((size_t)p.NCu * elem_len(r) * Bz * 8);
-  p.agg2_off = take((size_t)p.NCc * kWV * (r * r + r) * Bz * 8);
+  p.agg2_off = take((size_t)p.NCc * (r * r + r) * Bz * 8);
   p.total = off;
   return p;
 }
@@ -290,6 +315,33 @@ EKS_DEV void apply_map(const double (&G)[R][R], const double (&g)[R], double (&m
   for (int u = 0; u < R; ++u) ms[u] = nx[u];
 }
 
+// H <- F o H for affine maps (F applied after H): G = F.G H.G, g = F.G H.g + F.g
+template <int R>
+EKS_DEV void compose_map(const double (&FG)[R][R], const double (&Fg)[R], double (&HG)[R][R],
+                         double (&Hg)[R]) {
+  double G[R][R], g[R];
+#pragma unroll
+  for (int u = 0; u < R; ++u) {
+#pragma unroll
+    for (int v = 0; v < R; ++v) {
+      double t = 0.0;
+#pragma unroll
+      for (int q = 0; q < R; ++q) t = fma(FG[u][q], HG[q][v], t);
+      G[u][v] = t;
+    }
+    double t = Fg[u];
+#pragma unroll
+    for (int q = 0; q < R; ++q) t = fma(FG[u][q], Hg[q], t);
+    g[u] = t;
+  }
+#pragma unroll
+  for (int u = 0; u < R; ++u) {
+    Hg[u] = g[u];
+#pragma unroll
+    for (int v = 0; v < R; ++v) HG[u][v] = G[u][v];
+  }
+}
+
 // The first D steps of a lane's chunk into the ring (issued ahead: for the
 // next unit while the current one finishes its tail).
 template <int D, typename Src>
@@ -461,6 +513,8 @@ EKS_DEV unsigned k3_fwd_run(const SmoothArgs &a, const Plan3 &p, const Sched3 &s
   Work3 wk = decode3<0>(sc, t);  // uniform: every index below in SGPRs
   head(wk);
   while (wk.phase == 0) {
+    EKS_STAMP(0, 0);
+    EKS_STAMP(0, 1);
     unsigned tnext = 0;
     if (threadIdx.x == 0) tnext = atomicAdd(ctr, 1u);  // consumed after the streaming
     const long long cu = wk.c, grp = wk.grp;
@@ -544,8 +598,10 @@ EKS_DEV unsigned k3_fwd_run(const SmoothArgs &a, const Plan3 &p, const Sched3 &s
     } else {
       El.store(&shX[w][0][l], 64);
     }
+    EKS_STAMP(0, 2);
     if (threadIdx.x == 0) tk[(it + 1) & 1] = tnext;
     __syncthreads();
+    EKS_STAMP(0, 3);
     const unsigned tn = __builtin_amdgcn_readfirstlane(tk[(it + 1) & 1]);
     const Work3 wn = decode3<0>(sc, tn);
     // the next unit's first member steps in flight during this unit's tail
@@ -635,7 +691,9 @@ EKS_DEV unsigned k3_fwd_run(const SmoothArgs &a, const Plan3 &p, const Sched3 &s
       }
       head(wn);
     }
+    EKS_STAMP(0, 4);
     __syncthreads();
+    EKS_STAMP(0, 5);
     // fine start states: wave w's first chunk starts from the entering state
     // composed with the waves before it (slots 0 / 1 / 2 = X0 / X01 / X012;
     // wave 0's is the entering state itself, stored by the unit before), its
@@ -660,7 +718,9 @@ EKS_DEV unsigned k3_fwd_run(const SmoothArgs &a, const Plan3 &p, const Sched3 &s
     }
     if (lane_ok)
       flag(a.status, b, (ok ? 0 : EKS_STATUS_SCAN) | (okf ? 0 : EKS_STATUS_SINGULAR));
+    EKS_STAMP(0, 6);
     __syncthreads();  // LDS free for the next unit
+    EKS_STAMP(0, 7);
     t = tn;
     wk = wn;
     ++it;
@@ -719,7 +779,7 @@ template <int R, int N, int E, typename T, int AI, int CI, bool NLL, bool LB>
 EKS_DEV unsigned k3_bwd_run(const SmoothArgs &a, const Plan3 &p, const Sched3 &sc, unsigned t,
                             double *lds, unsigned *tk, unsigned *ctr, int &it) {
   constexpr int KS = R + Sym<R>::len, MP = R * R + R;
-  constexpr int D = kK3D;
+  constexpr int D = kK3BD;
   constexpr int NR = reg_steps3(R, N), NL = lds_steps3(R, N), LF = NR + NL;
   auto &fs = *reinterpret_cast<double (*)[NL][KS][64 * kWV]>(lds);  // filtered states, first NL steps
   auto &shM = *reinterpret_cast<double (*)[kWV - 1][MP][64]>(lds + NL * KS * 64 * kWV);  // maps of waves 1..3
@@ -734,41 +794,9 @@ EKS_DEV unsigned k3_bwd_run(const SmoothArgs &a, const Plan3 &p, const Sched3 &s
   const bool vec2 = N == 2 && a.oj == 1 && ((a.ob | a.ot) & 1) == 0 &&
                     (((uintptr_t)a.out) & 15) == 0;
   Work3 wk = decode3<1>(sc, t);  // uniform: every index below in SGPRs
-  // the member ring, persisting across the units of the run
-  typename SrcOf<E, N, T, D>::type src;
-  src.init(a);
-  // The head of unit wk_ for this wave: its model, the start state of its
-  // fine chunk and its first D member steps.  Issued for the next unit while
-  // this one runs its chain and backward sweep, so a unit starts with its
-  // loads landed instead of one HBM round trip of prologue.  Lanes past the
-  // last trajectory load trajectory 0 (wave-uniform branches only).
-  auto head = [&](const Work3 &wk_, Model<R, N> &md_, double (&m_)[R], double (&P_)[R][R]) {
-    if (wk_.phase != 1) return;
-    const long long f_ = (p.NCc - 1 - wk_.c) * kWV + w;
-    if (f_ >= p.NCf) return;
-    const unsigned b_ = (unsigned)(wk_.grp * 64 + l);
-    const unsigned bl_ = (long long)b_ < B ? b_ : 0u;
-    load_model_pl<R, N, AI, CI>(prm, B, bl_, f_ == 0, md_);
-    if (f_ == 0) {
-#pragma unroll
-      for (int i = 0; i < R; ++i) {
-        m_[i] = md_.m0[i];
-#pragma unroll
-        for (int j = 0; j < R; ++j) P_[i][j] = md_.S0[i][j];
-      }
-    } else {
-      load_state_pl<R>(fst, f_ * KS, B, bl_, m_, P_);
-    }
-    src.lane(a, bl_);
-    const long long s_ = f_ * p.L, e_ = min(TT, s_ + p.L);
-#pragma unroll
-    for (int q = 0; q < D; ++q)
-      if (s_ + q < e_) src.fetch(q, s_ + q);
-  };
-  Model<R, N> md;        // the current unit's model
-  double m[R], P[R][R];  // its fine chunk's start state, then the running filter state
-  head(wk, md, m, P);
   while (wk.phase == 1) {
+    EKS_STAMP(1, 0);
+    EKS_STAMP(1, 1);
     unsigned tnext = 0;
     if (tid == 0) tnext = atomicAdd(ctr, 1u);
     const long long cr = wk.c, grp = wk.grp;
@@ -778,6 +806,7 @@ EKS_DEV unsigned k3_bwd_run(const SmoothArgs &a, const Plan3 &p, const Sched3 &s
     const bool lane_ok = (long long)b < B;
     const bool live = lane_ok && f < p.NCf;
     bool ok = true, okc = true;  // recursions, and the chain wait
+    Model<R, N> md;
     // the last NR steps keep their RTS gains (J_t, d_t) from the forward
     // sweep in registers; the first NL keep filtered states in LDS
     double Jr[NR][R][R], dr[NR][R];
@@ -785,11 +814,30 @@ EKS_DEV unsigned k3_bwd_run(const SmoothArgs &a, const Plan3 &p, const Sched3 &s
     Mp.set_identity();
     const long long s = f * p.L, e = min(TT, s + p.L);
     // a whole fine chunk with a successor step after it (wave-uniform)
-    const bool full = e - s == LF && e < TT;
+    // (the single-view shape only: elsewhere the guarded loop, half the code)
+    const bool full = R == 2 && N == 2 && e - s == LF && e < TT;
     // wave-uniform branch: lanes past the last trajectory run on trajectory
     // 0's data and store nothing
     const unsigned bl = lane_ok ? b : 0u;
-    if (f < p.NCf) {  // (model, start state and first steps: head())
+    if (f < p.NCf) {
+      load_model_pl<R, N, AI, CI>(prm, B, bl, f == 0, md);
+      double m[R], P[R][R];
+      if (f == 0) {
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+          m[i] = md.m0[i];
+#pragma unroll
+          for (int j = 0; j < R; ++j) P[i][j] = md.S0[i][j];
+        }
+      } else {
+        load_state_pl<R>(fst, f * KS, B, bl, m, P);
+      }
+      typename SrcOf<E, N, T, D>::type src;
+      src.init(a);
+      src.lane(a, bl);
+#pragma unroll
+      for (int q = 0; q < D; ++q)
+        if (s + q < e) src.fetch(q, s + q);
       typename std::conditional<NLL, NllAcc, NoAcc>::type acc;  // NLL shares only when asked for
       // one forward step i (time tt) of the re-run.  FULL: a whole chunk that
       // is not the trajectory's last (every step present, every step has a
@@ -859,7 +907,7 @@ EKS_DEV unsigned k3_bwd_run(const SmoothArgs &a, const Plan3 &p, const Sched3 &s
 #pragma unroll
         for (int i = 0; i < LF; ++i) {
           fwd_step(i, s + i, std::true_type{});
-          __builtin_amdgcn_sched_barrier(0);  // one step's registers at a time
+          if constexpr (kK3BSched) __builtin_amdgcn_sched_barrier(0);  // one step's registers at a time
         }
       } else {
 #pragma unroll
@@ -878,6 +926,7 @@ EKS_DEV unsigned k3_bwd_run(const SmoothArgs &a, const Plan3 &p, const Sched3 &s
         Mp.set_identity();
       }
     }
+    EKS_STAMP(1, 2);
     if (w >= 1) {
       int k = 0;
 #pragma unroll
@@ -887,27 +936,42 @@ EKS_DEV unsigned k3_bwd_run(const SmoothArgs &a, const Plan3 &p, const Sched3 &s
 #pragma unroll
       for (int u = 0; u < R; ++u) shM[w - 1][k++][l] = Mp.g[u];
     }
-    if (tid == 0) tk[(it + 1) & 1] = tnext;
     __syncthreads();
-    // the next unit (its ticket taken at this unit's start): its head is
-    // loaded during this unit's chain and backward sweep -- waves 1-3 now,
-    // wave 0 after its chain wait (vmcnt counts in order: a prefetch issued
-    // before the poll would hold the poll back until it lands)
-    const unsigned tn = __builtin_amdgcn_readfirstlane(tk[(it + 1) & 1]);
-    const Work3 wn = decode3<1>(sc, tn);
-    Model<R, N> mdn;
-    double mn[R], Pn[R][R];
-    if (w != 0) head(wn, mdn, mn, Pn);
+    EKS_STAMP(1, 3);
     double ms[R];  // smoothed mean at the first step after this chunk
     if (w == 0) {
       // the chain: the mean at the first step of coarse chunk cc+1, published
       // by its unit (for the last coarse chunk: unused, its last map is
-      // constant).  Decoupled look-back as in k3_fwd: if unit cc+1 has not
-      // published it yet, this unit publishes its 4 maps for the units before
-      // it, walks forward to the nearest unit j with a published mean and
-      // carries that mean back through the maps of units j-1 .. cc+1, right
-      // to left, with the expression the units themselves use (apply_map):
-      // the same bits whichever j it starts from.
+      // constant).  The unit's map U = M0 o M1 o M2 o M3 (its 4 chunk maps,
+      // composed right to left in a fixed order) carries that mean to the
+      // mean at the unit's first step, which the unit publishes.  Decoupled
+      // look-back as in k3_fwd: if unit cc+1 has not published its mean yet,
+      // this unit publishes U for the units before it, walks forward to the
+      // nearest unit j with a published mean and carries that mean back
+      // through the maps U of units j-1 .. cc+1 with the expression every
+      // unit uses (apply_map): the same bits whichever j it starts from.
+      // The walk's loads go out KLB units at a time (one round trip per KLB
+      // units instead of one per chunk map).
+      constexpr int KLB = 4;
+      double UG[R][R], Ug[R];
+#pragma unroll
+      for (int u = 0; u < R; ++u) {
+        Ug[u] = shM[kWV - 2][R * R + u][l];
+#pragma unroll
+        for (int v = 0; v < R; ++v) UG[u][v] = shM[kWV - 2][u * R + v][l];
+      }
+#pragma unroll
+      for (int v = kWV - 2; v >= 1; --v) {
+        double G[R][R], g[R];
+#pragma unroll
+        for (int u = 0; u < R; ++u) {
+          g[u] = shM[v - 1][R * R + u][l];
+#pragma unroll
+          for (int q = 0; q < R; ++q) G[u][q] = shM[v - 1][u * R + q][l];
+        }
+        compose_map<R>(G, g, UG, Ug);
+      }
+      compose_map<R>(Mp.G, Mp.g, UG, Ug);
 #pragma unroll
       for (int u = 0; u < R; ++u) ms[u] = 0.0;
       if (cc + 1 < p.NCc) {
@@ -918,19 +982,12 @@ EKS_DEV unsigned k3_bwd_run(const SmoothArgs &a, const Plan3 &p, const Sched3 &s
         } else if (!inc_ready(fl + j, a.wait_ticks)) {
           if (cc > 0) {
             if (lane_ok) {
-              double *mp0 = agg2;
-              const long long base = cc * kWV * MP;
 #pragma unroll
               for (int u = 0; u < R; ++u) {
 #pragma unroll
-                for (int q = 0; q < R; ++q) st_wt(&pl(mp0, base + u * R + q, B, b), Mp.G[u][q]);
-                st_wt(&pl(mp0, base + R * R + u, B, b), Mp.g[u]);
+                for (int q = 0; q < R; ++q) st_wt(&pl(agg2, cc * MP + u * R + q, B, b), UG[u][q]);
+                st_wt(&pl(agg2, cc * MP + R * R + u, B, b), Ug[u]);
               }
-#pragma unroll
-              for (int v = 1; v < kWV; ++v)
-#pragma unroll
-                for (int k = 0; k < MP; ++k)
-                  st_wt(&pl(mp0, base + v * MP + k, B, b), shM[v - 1][k][l]);
             }
             publish_flag(flags + grp * p.NCc + cc, l, kAggReady);
           }
@@ -939,23 +996,28 @@ EKS_DEV unsigned k3_bwd_run(const SmoothArgs &a, const Plan3 &p, const Sched3 &s
         if (lane_ok) {
 #pragma unroll
           for (int u = 0; u < R; ++u) ms[u] = ld_wt(&pl(inc, j * R + u, B, b));
-          for (long long i = j - 1; i > cc; --i) {
+          for (long long i0 = j - 1; i0 > cc; i0 -= KLB) {
+            double G[KLB][R][R], g[KLB][R];
 #pragma unroll
-            for (int v = kWV - 1; v >= 0; --v) {
-              double G[R][R], g[R];
-              const long long base = (i * kWV + v) * MP;
+            for (int k = 0; k < KLB; ++k) {
+              const long long i = i0 - k > cc ? i0 - k : i0;  // (past cc: a re-load, unused)
 #pragma unroll
               for (int u = 0; u < R; ++u) {
 #pragma unroll
-                for (int q = 0; q < R; ++q) G[u][q] = ld_wt(&pl(agg2, base + u * R + q, B, b));
-                g[u] = ld_wt(&pl(agg2, base + R * R + u, B, b));
+                for (int q = 0; q < R; ++q) G[k][u][q] = ld_wt(&pl(agg2, i * MP + u * R + q, B, b));
+                g[k][u] = ld_wt(&pl(agg2, i * MP + R * R + u, B, b));
               }
-              apply_map<R>(G, g, ms);
             }
+#pragma unroll
+            for (int k = 0; k < KLB; ++k)
+              if (i0 - k > cc) apply_map<R>(G[k], g[k], ms);
           }
         }
       }
       // right to left through waves 3, 2, 1: hand each its entering mean
+      double mnext[R];
+#pragma unroll
+      for (int u = 0; u < R; ++u) mnext[u] = ms[u];
 #pragma unroll
       for (int v = kWV - 1; v >= 1; --v) {
         double G[R][R], g[R];
@@ -970,19 +1032,17 @@ EKS_DEV unsigned k3_bwd_run(const SmoothArgs &a, const Plan3 &p, const Sched3 &s
         for (int u = 0; u < R; ++u) shM[v - 1][u][l] = ms[u];
         apply_map<R>(G, g, ms);
       }
-      if (cc > 0) {  // the mean at this coarse chunk's first step
-        double x[R];
-#pragma unroll
-        for (int u = 0; u < R; ++u) x[u] = ms[u];
-        apply_map<R>(Mp.G, Mp.g, x);
+      if (cc > 0) {  // the mean at this coarse chunk's first step: U(mean entering the unit)
+        apply_map<R>(UG, Ug, mnext);
         if (lane_ok)
 #pragma unroll
-          for (int u = 0; u < R; ++u) st_wt(&pl(inc, cc * R + u, B, b), x[u]);
+          for (int u = 0; u < R; ++u) st_wt(&pl(inc, cc * R + u, B, b), mnext[u]);
         publish_flag(flags + grp * p.NCc + cc, l, kIncReady);
       }
-      head(wn, mdn, mn, Pn);
     }
+    EKS_STAMP(1, 4);
     __syncthreads();
+    EKS_STAMP(1, 5);
     if (w >= 1)
 #pragma unroll
       for (int u = 0; u < R; ++u) ms[u] = shM[w - 1][u][l];
@@ -1085,18 +1145,14 @@ EKS_DEV unsigned k3_bwd_run(const SmoothArgs &a, const Plan3 &p, const Sched3 &s
           if (s + i < e) bwd_lds(i, s + i);
       }
     }
+    EKS_STAMP(1, 6);
     if (lane_ok)
       flag(a.status, b, (ok ? 0 : EKS_STATUS_SINGULAR) | (okc ? 0 : EKS_STATUS_SCAN));
-    __syncthreads();  // LDS free for the next unit
-    md = mdn;
-#pragma unroll
-    for (int i = 0; i < R; ++i) {
-      m[i] = mn[i];
-#pragma unroll
-      for (int j = 0; j < R; ++j) P[i][j] = Pn[i][j];
-    }
-    t = tn;
-    wk = wn;
+    if (tid == 0) tk[(it + 1) & 1] = tnext;
+    __syncthreads();  // LDS free for the next unit, its ticket visible
+    EKS_STAMP(1, 7);
+    t = __builtin_amdgcn_readfirstlane(tk[(it + 1) & 1]);
+    wk = decode3<1>(sc, t);
     ++it;
   }
   return t;
@@ -1172,25 +1228,23 @@ int launch_algo3_one(const SmoothArgs &a) {
       // single-view shape
       bool lb = false;
       if constexpr (kSingleView) lb = a3_bwd_lookback(p);
-      if (a.nll) {
-        if (lb)
-          hipLaunchKernelGGL((k3_bwd<R, N, EE, Tp, AI, CI, true, true>),
-                             dim3(persistent_grid<k3_bwd<R, N, EE, Tp, AI, CI, true, true>>(p.units)),
-                             dim3(64 * kWV), 0, a.stream, a, p, sb);
-        else
-          hipLaunchKernelGGL((k3_bwd<R, N, EE, Tp, AI, CI, true, false>),
-                             dim3(persistent_grid<k3_bwd<R, N, EE, Tp, AI, CI, true, false>>(p.units)),
-                             dim3(64 * kWV), 0, a.stream, a, p, sb);
-      } else {
-        if (lb)
-          hipLaunchKernelGGL((k3_bwd<R, N, EE, Tp, AI, CI, false, true>),
-                             dim3(persistent_grid<k3_bwd<R, N, EE, Tp, AI, CI, false, true>>(p.units)),
-                             dim3(64 * kWV), 0, a.stream, a, p, sb);
-        else
-          hipLaunchKernelGGL((k3_bwd<R, N, EE, Tp, AI, CI, false, false>),
-                             dim3(persistent_grid<k3_bwd<R, N, EE, Tp, AI, CI, false, false>>(p.units)),
-                             dim3(64 * kWV), 0, a.stream, a, p, sb);
-      }
+      // (the look-back instantiation exists for the single-view shape only)
+      auto bwd = [&](auto nll, auto lbc) {
+        constexpr bool NL_ = decltype(nll)::value, LB_ = decltype(lbc)::value;
+        hipLaunchKernelGGL((k3_bwd<R, N, EE, Tp, AI, CI, NL_, LB_>),
+                           dim3(persistent_grid<k3_bwd<R, N, EE, Tp, AI, CI, NL_, LB_>>(p.units)),
+                           dim3(64 * kWV), 0, a.stream, a, p, sb);
+      };
+      auto bwd_nll = [&](auto nll) {
+        if constexpr (kSingleView) {
+          if (lb) bwd(nll, std::true_type{});
+          else bwd(nll, std::false_type{});
+        } else {
+          bwd(nll, std::false_type{});
+        }
+      };
+      if (a.nll) bwd_nll(std::true_type{});
+      else bwd_nll(std::false_type{});
       if ((rc = check_launch("k3_bwd"))) return rc;
     }
     if (a.nll) {

@@ -1,6 +1,8 @@
-"""Phase breakdown of k3_bwd from in-kernel s_memtime stamps (experiment
-build exp/stamps: exp/stamps.patch).  Runs config 4 (or --videos N) eagerly,
-copies the stamps of the last call and prints mean cycles per phase."""
+"""Phase breakdown of algo 3's passes from in-kernel s_memtime stamps
+(profiling build: tools/build_cur.sh stamps -DEKS_STAMPS=1 eks_shape_22.hip,
+then EKS_LIB=exp/stamps/libeks_hip.so).  Runs config 4 (or --videos N)
+eagerly, copies the stamps of the last call and prints the mean cycles of
+each phase per wave (two_pass.hpp EKS_STAMP points)."""
 import ctypes as C
 import os
 import sys
@@ -13,6 +15,10 @@ import bench  # noqa: E402
 import torch  # noqa: E402
 from eks_amd import _lib  # noqa: E402
 
+BLK, ITS = 512, 128
+NAMES = {0: ["stream", "bar1", "chain(w0)", "bar2", "starts", "bar3"],
+         1: ["fwd sweep", "bar1", "chain(w0)", "bar2", "bwd sweep", "bar3"]}
+
 a = bench.parse()
 dev = torch.device("cuda", 0)
 torch.cuda.set_device(0)
@@ -21,37 +27,27 @@ for _ in range(3):
     w["step"]()
 torch.cuda.synchronize()
 lib = _lib.load()
-n = 512 * 128 * 32
-buf = np.zeros(n, dtype=np.uint64)
+buf = np.zeros(2 * BLK * ITS * 32, dtype=np.uint64)
 lib.eks_dbg_stamps.restype = C.c_int
-rc = lib.eks_dbg_stamps(buf.ctypes.data_as(C.c_void_p), C.c_size_t(buf.nbytes))
-assert rc == 0, rc
-st = buf.reshape(512, 128, 4, 8).astype(np.int64)
-names = ["fwd sweep", "bar1", "chain(w0)", "bar2", "bwd sweep", "bar3"]
-rows = []
-for blk in range(512):
-    for it in range(128):
-        s = st[blk, it]
-        if s[0, 1] == 0:
-            continue
-        rows.append(s)
-rows = np.array(rows)  # (units, 4 waves, 8)
-print("units stamped", len(rows))
-tot = rows[:, :, 7] - rows[:, :, 1]
-for wv in range(4):
-    d = [rows[:, wv, k + 1] - rows[:, wv, k] for k in range(1, 7)]
-    print(f"wave {wv}: " + "  ".join(f"{nm}={np.mean(x):8.0f}" for nm, x in zip(names, d)) +
-          f"  total={np.mean(tot[:, wv]):8.0f} cyc")
-# gaps between units of one block (ticket decode, loop back)
-gaps = []
-for blk in range(512):
-    s = st[blk]
-    its = [i for i in range(128) if s[i, 0, 1] != 0]
-    for i0, i1 in zip(its, its[1:]):
-        gaps.append(s[i1, 0, 1] - s[i0, 0, 7])
-print("gap between units (w0)", np.mean(gaps) if gaps else None)
-# chain wait distribution (wave 0)
-ch = rows[:, 0, 4] - rows[:, 0, 3]
-print("chain w0 percentiles", np.percentile(ch, [10, 50, 90, 99]))
-fw = rows[:, 0, 2] - rows[:, 0, 1]
-print("fwd w0 percentiles", np.percentile(fw, [10, 50, 90, 99]))
+assert lib.eks_dbg_stamps(buf.ctypes.data_as(C.c_void_p), C.c_size_t(buf.nbytes)) == 0
+st = buf.reshape(2, BLK, ITS, 4, 8).astype(np.int64)
+for ps, kern in ((0, "k3_fwd"), (1, "k3_bwd")):
+    rows = st[ps][st[ps][:, :, 0, 1] != 0]  # (units, 4 waves, 8)
+    print(f"{kern}: units stamped {len(rows)}")
+    if not len(rows):
+        continue
+    tot = rows[:, :, 7] - rows[:, :, 1]
+    for wv in range(4):
+        d = [rows[:, wv, k + 1] - rows[:, wv, k] for k in range(1, 7)]
+        print(f"  wave {wv}: " + "  ".join(f"{nm}={np.mean(x):7.0f}" for nm, x in zip(NAMES[ps], d))
+              + f"  total={np.mean(tot[:, wv]):7.0f} cyc")
+    gaps = []
+    for blk in range(BLK):
+        s = st[ps, blk]
+        its = [i for i in range(ITS) if s[i, 0, 1] != 0]
+        gaps += [s[i1, 0, 1] - s[i0, 0, 7] for i0, i1 in zip(its, its[1:])]
+    print("  gap between a block's units (w0):", np.percentile(gaps, [10, 50, 90]) if gaps else None)
+    ch = rows[:, 0, 4] - rows[:, 0, 3]
+    print("  chain w0 percentiles 10/50/90/99:", np.percentile(ch, [10, 50, 90, 99]))
+    fw = rows[:, 0, 2] - rows[:, 0, 1]
+    print("  first phase w0 percentiles 10/50/90/99:", np.percentile(fw, [10, 50, 90, 99]))
