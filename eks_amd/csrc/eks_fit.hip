@@ -363,8 +363,16 @@ EKS_DEV K block_select(const K *keys, long long n, long long k, int top,
 constexpr int kCand = 3072;        // LDS candidates (24 KB + 6 KB of indices)
 constexpr int kSelDigit = 8;       // digits of the in-LDS select (1 KB histogram)
 constexpr long long kLdsMaskT = 65536;  // rows with 16-bit frame indices
+// keys per thread of the register-resident selection (256 threads: rows up
+// to 10 240 frames, config 4's 10 000)
+constexpr int kSelKPT = 40;
 
-template <int BLK>
+// KPT > 0 (rows of at most BLK * KPT frames): the row is read ONCE, into
+// KPT registers per thread, and both passes (histogram, compaction + mask)
+// run over the registers -- round 4's form read the row from memory twice
+// (1.93x the worst plane's bytes at config 4).  KPT = 0: the passes read
+// the row from memory (longer rows).
+template <int BLK, int KPT = 0>
 __global__ __launch_bounds__(BLK) void k_fit_select(const double *__restrict__ worst,
                                                     long long TT, long long lo, long long hi,
                                                     double g, double *__restrict__ thr,
@@ -391,6 +399,32 @@ __global__ __launch_bounds__(BLK) void k_fit_select(const double *__restrict__ w
   const uint64_t *keys = reinterpret_cast<const uint64_t *>(worst + b * TT);
   uint64_t *krow = kept ? kept + b * W : nullptr;
   constexpr int lo_bit = 51;
+  // the row's keys in registers (KPT > 0): key threadIdx.x + u * BLK in
+  // xr[u]; every load issued at once.  Past the row: +inf bit patterns
+  // above every variance (never counted: the loops below test the index).
+  constexpr int KR = KPT > 0 ? KPT : 1;
+  uint64_t xr[KR];
+  if constexpr (KPT > 0) {
+#pragma unroll
+    for (int u = 0; u < KPT; ++u) {
+      const long long i = threadIdx.x + (long long)u * BLK;
+      xr[u] = i < TT ? keys[i] : ~0ull;
+    }
+  }
+  // f(key, index) over the row: from the registers, or from memory
+  auto row_keys = [&](auto &&f) {
+    if constexpr (KPT > 0) {
+#pragma unroll
+      for (int u = 0; u < KPT; ++u) {
+        const long long i = threadIdx.x + (long long)u * BLK;
+        // whole waves run each u (indices of a wave are 64-aligned): the
+        // ballots inside f see the wave's 64 frames, past-the-row lanes false
+        if ((long long)(threadIdx.x & ~63u) + (long long)u * BLK < TT) f(xr[u], i, i < TT);
+      }
+    } else {
+      for_keys<BLK>(keys, TT, [&](uint64_t x, long long i) { f(x, i, true); });
+    }
+  };
   for (unsigned i = threadIdx.x; i < (kPacked ? kBins / 2 : kBins); i += BLK) hist[i] = 0;
   if (threadIdx.x == 0) {
     any_nan = 0;
@@ -399,7 +433,8 @@ __global__ __launch_bounds__(BLK) void k_fit_select(const double *__restrict__ w
   __syncthreads();
   // pass 1: NaN check + top-digit histogram
   bool nan = false;
-  for_keys<BLK>(keys, TT, [&](uint64_t x, long long) {
+  row_keys([&](uint64_t x, long long, bool valid) {
+    if (!valid) return;
     nan |= (x & 0x7fffffffffffffffull) > 0x7ff0000000000000ull;
     const unsigned d = (unsigned)(x >> lo_bit) & (kBins - 1);
     if constexpr (kPacked)
@@ -444,12 +479,12 @@ __global__ __launch_bounds__(BLK) void k_fit_select(const double *__restrict__ w
   if (in_lds) {
     // pass 2: compact the bin into LDS; mask words of the frames below it
     // wave-aggregated slot allocation: one LDS atomic per wave and key batch
-    for_keys<BLK>(keys, TT, [&](uint64_t x, long long i) {
+    row_keys([&](uint64_t x, long long i, bool valid) {
       if (lds_mask) {
-        const uint64_t mb = __ballot(x < binpfx);  // below the bin: kept
+        const uint64_t mb = __ballot(valid && x < binpfx);  // below the bin: kept
         if (first_active_lane()) smask[i >> 6] = mb;
       }
-      const bool in = (x & binmask) == binpfx;
+      const bool in = valid && (x & binmask) == binpfx;
       const uint64_t m = __ballot(in);
       if (m == 0) return;
       const int lane = threadIdx.x & 63;
@@ -1002,28 +1037,40 @@ __global__ __launch_bounds__(256) void k_fit_accum(const T *__restrict__ obs, Fi
     if (t1 > t0)
 #pragma unroll
       for (int q = 0; q < kAccD; ++q) fetch(q, t0 + q);
-    // the mask word of the current 64 frames, and the next one loaded a word
-    // ahead (vmcnt counts in order: a word loaded just before its use would
-    // drain the ring's loads issued before it)
-    const long long w0 = t0 >> 6;
-    uint64_t m = t1 > t0 ? krow[w0] : 0ull;
-    uint64_t mn = w0 + 1 < W ? krow[w0 + 1] : 0ull;
-    for (long long tb = t0; tb < t1; tb += kAccD) {
+    // whole blocks of kAccD frames as straight-line code (no per-frame
+    // guard: the waitcnt pass then counts the ring's loads exactly instead of
+    // draining them at every frame).  t0 is a multiple of 16, so a block never
+    // straddles a mask word; the word of the NEXT block is loaded at the top
+    // of each block, ahead of that block's ring loads (vmcnt counts in issue
+    // order: a word loaded just before its use would drain the ring)
+    const long long wl = (t1 - 1) >> 6;  // the chunk's last mask word
+    uint64_t m = krow[t0 >> 6];
+    long long tb = t0;
+    // (unrolled 8 x: the waitcnt pass loses count of the ring at a loop
+    // back-edge and drains it there, so take one back-edge per 64 frames)
+#pragma unroll 8
+    for (; tb + kAccD <= t1; tb += kAccD) {
+      const long long wn = (tb + kAccD) >> 6;
+      const uint64_t mnext = krow[wn < wl ? wn : wl];
 #pragma unroll
       for (int q = 0; q < kAccD; ++q) {
-        const long long t = tb + q;
-        if (t < t1) {
-          if (t > t0 && (t & 63) == 0) {
-            m = mn;
-            mn = (t >> 6) + 1 < W ? krow[(t >> 6) + 1] : 0ull;
-          }
+        double y[N];
+#pragma unroll
+        for (int j = 0; j < N; ++j) y[j] = (double)ring[q][j];
+        fetch(q, tb + q + kAccD);
+        if ((m >> ((tb + q) & 63)) & 1ull) take(y);
+      }
+      m = mnext;
+    }
+    if (tb < t1) {  // the chunk's last frames (fewer than kAccD)
+#pragma unroll
+      for (int q = 0; q < kAccD; ++q)
+        if (tb + q < t1) {
           double y[N];
 #pragma unroll
           for (int j = 0; j < N; ++j) y[j] = (double)ring[q][j];
-          fetch(q, t + kAccD);
-          if ((m >> (t & 63)) & 1ull) take(y);
+          if ((m >> ((tb + q) & 63)) & 1ull) take(y);
         }
-      }
     }
   } else if constexpr (FROM_YEV) {
     // WAVE_MERGE (few long trajectories, a wave = 64 chunks of one
@@ -1581,62 +1628,72 @@ __global__ __launch_bounds__(256) void k_fitw_accum(const T *__restrict__ obs, F
     }
 }
 
-// k_fit_final's PCA model for n = 10..16 (even): one 256-thread block per
-// trajectory, thread (i, j) = (L / 16, L % 16) owning entry (i, j); the
-// round-robin Jacobi's cross-entry reads go through LDS
+// k_fit_final's PCA model for n = 10..16 (even): ONE WAVE per trajectory,
+// lane L owning entries (i, j0 .. j0 + 3) of the n x n matrix, i = L / 4,
+// j0 = 4 (L % 4); the round-robin Jacobi's cross-entry reads go through LDS
+// (a one-wave workgroup: its barriers are free).  Round 4's form used 256
+// threads (one entry each) and 4-wave barriers twice per rotation round,
+// ~90 us at 6 cameras for 17 trajectories, bound by those barriers.  The
+// rotation arithmetic per entry is unchanged; the sweep's convergence sums
+// add the same squares in another order.
+constexpr int kFwEnt = kNW * kNW / 64;  // entries per lane
 template <int R>
-__global__ __launch_bounds__(256) void k_fitw_final(long long B, const double *__restrict__ part,
-                                                    FitShift ks, int n, double smooth_param,
-                                                    double *__restrict__ params,
-                                                    int32_t *__restrict__ status) {
+__global__ __launch_bounds__(64) void k_fitw_final(long long B, const double *__restrict__ part,
+                                                   FitShift ks, int n, double smooth_param,
+                                                   double *__restrict__ params,
+                                                   int32_t *__restrict__ status) {
   __shared__ double sA[kNW * kNW], sV[kNW * kNW], sM[kNW * kNW], sD[kNW * kNW], sEv[kNW];
-  __shared__ double sRed[2][4];
   const CsRt CS(n);
   const long long b = blockIdx.x;
-  const int L = threadIdx.x, i = L / kNW, j = L % kNW;
-  const bool own = i < n && j < n;
+  const int L = threadIdx.x, i = L / (kNW / kFwEnt), j0 = (L % (kNW / kFwEnt)) * kFwEnt;
   const double *o = part + b * CS.kLen;
   const double cnt = o[CS.cnt];
   double np_ = o[CS.npair];
   if (np_ < 1.0) np_ = __builtin_nan("");
-  const int ti = own ? (i <= j ? CS.tri(i, j) : CS.tri(j, i)) : 0;
-  const double s1i = own ? o[CS.mean + i] : 0.0, s1j = own ? o[CS.mean + j] : 0.0;
-  const double d1i = own ? o[CS.dmean + i] : 0.0, d1j = own ? o[CS.dmean + j] : 0.0;
-  const double Mij = own ? o[CS.M + ti] - s1i * (s1j / cnt) : 0.0;
-  const double Dij = own ? o[CS.dM + ti] - d1i * (d1j / np_) : 0.0;
+  double a[kFwEnt], v[kFwEnt], Mij[kFwEnt], Dij[kFwEnt];
+  bool own[kFwEnt];
+#pragma unroll
+  for (int u = 0; u < kFwEnt; ++u) {
+    const int j = j0 + u;
+    own[u] = i < n && j < n;
+    const int ti = own[u] ? (i <= j ? CS.tri(i, j) : CS.tri(j, i)) : 0;
+    const double s1i = own[u] ? o[CS.mean + i] : 0.0, s1j = own[u] ? o[CS.mean + j] : 0.0;
+    const double d1i = own[u] ? o[CS.dmean + i] : 0.0, d1j = own[u] ? o[CS.dmean + j] : 0.0;
+    Mij[u] = own[u] ? o[CS.M + ti] - s1i * (s1j / cnt) : 0.0;
+    Dij[u] = own[u] ? o[CS.dM + ti] - d1i * (d1j / np_) : 0.0;
+    a[u] = Mij[u];
+    v[u] = (own[u] && i == j) ? 1.0 : 0.0;
+  }
   // packed row [m0 | S0 | A | Q | C (n x R) | offset (n)]
   const int pS0 = R, pA = R + R * R, pQ = R + 2 * R * R, pC = R + 3 * R * R, pOff = pC + n * R;
   double *pr = params + b * (long long)(pOff + n);
   if (L < R) pr[L] = 0.0;
   if (L < R * R) pr[pA + L] = (L / R == L % R) ? 1.0 : 0.0;
   if (L < n) pr[pOff + L] = ks.K[b * n + L] + o[CS.mean + L] / cnt;
-  double a = Mij, v = (own && i == j) ? 1.0 : 0.0;
   const int Nm = n - 1;
   auto slot_of = [&](int x, int k) { return x == 0 ? 0 : 1 + (x - 1 + Nm - (k % Nm)) % Nm; };
   auto idx_at = [&](int pos, int k) { return pos == 0 ? 0 : 1 + (pos - 1 + k) % Nm; };
   for (int sweep = 0; sweep < 60; ++sweep) {
-    double off = (own && i < j) ? a * a : 0.0, dia = (own && i == j) ? a * a : 0.0;
+    double off = 0.0, dia = 0.0;
+#pragma unroll
+    for (int u = 0; u < kFwEnt; ++u) {
+      off += (own[u] && i < j0 + u) ? a[u] * a[u] : 0.0;
+      dia += (own[u] && i == j0 + u) ? a[u] * a[u] : 0.0;
+    }
 #pragma unroll
     for (int w = 32; w >= 1; w >>= 1) {
       off += __shfl_xor(off, w, 64);
       dia += __shfl_xor(dia, w, 64);
     }
-    if ((L & 63) == 0) {
-      sRed[0][L >> 6] = off;
-      sRed[1][L >> 6] = dia;
-    }
-    __syncthreads();
-    off = sRed[0][0] + sRed[0][1] + sRed[0][2] + sRed[0][3];
-    dia = sRed[1][0] + sRed[1][1] + sRed[1][2] + sRed[1][3];
-    __syncthreads();
-    if (off == 0.0 || off <= 1e-34 * dia) break;  // block-uniform
+    if (off == 0.0 || off <= 1e-34 * dia) break;  // wave-uniform
     for (int k = 0; k < Nm; ++k) {
-      sA[L] = a;
-      sV[L] = v;
+#pragma unroll
+      for (int u = 0; u < kFwEnt; ++u) {
+        sA[i * kNW + j0 + u] = a[u];
+        sV[i * kNW + j0 + u] = v[u];
+      }
       __syncthreads();
       auto partner = [&](int x) { return idx_at(Nm - slot_of(x, k), k); };
-      const int li = own ? i : 0, lj = own ? j : 0;
-      const int pi = partner(li), pj = partner(lj);
       auto rot = [&](int x, int px, double &jxx, double &jpx) {
         const int p = x < px ? x : px, q = x < px ? px : x;
         const double apq = sA[p * kNW + q], app = sA[p * kNW + p], aqq = sA[q * kNW + q];
@@ -1650,24 +1707,38 @@ __global__ __launch_bounds__(256) void k_fitw_final(long long B, const double *_
         jxx = cs;
         jpx = x == p ? -sn : sn;
       };
-      double ji, jpi_i, jj, jpj_j;
+      const int li = i < n ? i : 0, pi = partner(li);
+      double ji, jpi_i;
       rot(li, pi, ji, jpi_i);
-      rot(lj, pj, jj, jpj_j);
-      const double a_ipj = sA[li * kNW + pj], a_pij = sA[pi * kNW + lj];
-      const double a_pipj = sA[pi * kNW + pj], v_ipj = sV[li * kNW + pj];
-      __syncthreads();
-      if (own) {
-        const double r0 = a * jj + a_ipj * jpj_j;
+      double na[kFwEnt], nv[kFwEnt];
+#pragma unroll
+      for (int u = 0; u < kFwEnt; ++u) {
+        const int lj = own[u] ? j0 + u : 0, pj = partner(lj);
+        double jj, jpj_j;
+        rot(lj, pj, jj, jpj_j);
+        const double a_ipj = sA[li * kNW + pj], a_pij = sA[pi * kNW + lj];
+        const double a_pipj = sA[pi * kNW + pj], v_ipj = sV[li * kNW + pj];
+        const double r0 = a[u] * jj + a_ipj * jpj_j;
         const double r1 = a_pij * jj + a_pipj * jpj_j;
-        a = ji * r0 + jpi_i * r1;
-        v = v * jj + v_ipj * jpj_j;
+        na[u] = own[u] ? ji * r0 + jpi_i * r1 : a[u];
+        nv[u] = own[u] ? v[u] * jj + v_ipj * jpj_j : v[u];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < kFwEnt; ++u) {
+        a[u] = na[u];
+        v[u] = nv[u];
       }
     }
   }
-  sV[L] = v;
-  sM[L] = Mij;
-  sD[L] = Dij;
-  if (own && i == j) sEv[i] = a;
+#pragma unroll
+  for (int u = 0; u < kFwEnt; ++u) {
+    const int e = i * kNW + j0 + u;
+    sV[e] = v[u];
+    sM[e] = Mij[u];
+    sD[e] = Dij[u];
+    if (own[u] && i == j0 + u) sEv[i] = a[u];
+  }
   __syncthreads();
   int order[R];
   unsigned used = 0;
@@ -1697,11 +1768,15 @@ __global__ __launch_bounds__(256) void k_fitw_final(long long B, const double *_
     pr[pS0 + L] = k == l ? s0 / cnt : 0.0;
     pr[pQ + L] = smooth_param * (q / (np_ - 1.0));
   }
-  if (own && j < R) {
-    int oj = 0;
 #pragma unroll
-    for (int u = 0; u < R; ++u) oj = u == j ? order[u] : oj;
-    pr[pC + i * R + j] = sV[i * kNW + oj];
+  for (int u = 0; u < kFwEnt; ++u) {
+    const int j = j0 + u;
+    if (own[u] && j < R) {
+      int oj = 0;
+#pragma unroll
+      for (int w = 0; w < R; ++w) oj = w == j ? order[w] : oj;
+      pr[pC + i * R + j] = sV[i * kNW + oj];
+    }
   }
   if (status && L == 0) status[b] = cnt > 0.0 ? 0 : EKS_STATUS_SINGULAR;
 }
@@ -1855,6 +1930,12 @@ extern "C" int eks_fit(const void *obs, int obs_dtype, int64_t B, int64_t T, int
     } else if (T >= 65536) {
       hipLaunchKernelGGL(k_fit_select<1024>, dim3((unsigned)B), dim3(1024), 0, s, worst, T,
                          lo, hi, g, thr, yev ? kept : nullptr, W);
+    } else if (T <= 256 * 16) {  // the row read once, into registers
+      hipLaunchKernelGGL((k_fit_select<256, 16>), dim3((unsigned)B), dim3(256), 0, s, worst, T, lo,
+                         hi, g, thr, yev ? kept : nullptr, W);
+    } else if (T <= 256 * kSelKPT) {
+      hipLaunchKernelGGL((k_fit_select<256, kSelKPT>), dim3((unsigned)B), dim3(256), 0, s, worst, T,
+                         lo, hi, g, thr, yev ? kept : nullptr, W);
     } else {
       hipLaunchKernelGGL(k_fit_select<256>, dim3((unsigned)B), dim3(256), 0, s, worst, T, lo,
                          hi, g, thr, yev ? kept : nullptr, W);
@@ -1915,7 +1996,7 @@ extern "C" int eks_fit(const void *obs, int obs_dtype, int64_t B, int64_t T, int
       double *src = merge(ic<0>{}, npart);
       if (!src) return EKS_ERR_HIP;
       prof_mark(s, "k_fitw_final");
-      hipLaunchKernelGGL((k_fitw_final<3>), dim3((unsigned)B), dim3(256), 0, s, B, src, ks, n,
+      hipLaunchKernelGGL((k_fitw_final<3>), dim3((unsigned)B), dim3(64), 0, s, B, src, ks, n,
                          smooth_param, params, status);
       prof_call_end(s);
       return check_launch("k_fitw_final");

@@ -124,6 +124,14 @@ EKS_DEV bool inc_ready(const unsigned *flag, long long wait_ticks) {
   acquire_after_poll();
   return true;
 }
+// the same with a flag word polled earlier (v, any lane's copy: the word is
+// wave-uniform); false when it did not say "inclusive published" yet
+EKS_DEV bool inc_ready_early(unsigned v, long long wait_ticks) {
+  if (wait_ticks < 0) return false;  // fault injection: always look back
+  if ((unsigned)__builtin_amdgcn_readfirstlane(v) < kIncReady) return false;
+  acquire_after_poll();
+  return true;
+}
 EKS_DEV long long look_back(const unsigned *flags, long long j, long long stride, int step,
                             long long nunits, long long wait_ticks, bool &ok) {
   if (wait_ticks < 0) {  // fault injection (tests): give up at once

@@ -24,13 +24,39 @@ constexpr bool kNtOut = true;
 #endif
 constexpr bool kHandoffFences = EKS_HANDOFF_FENCES != 0;
 
-// member prefetch distance (steps) of both algo-3 passes (k3_bwd: its own,
-// A/B-able with -DEKS_K3B_D=...)
+// member prefetch distance (steps) of both algo-3 passes; k3_bwd its own
+// (config 4, one box: k3_bwd 1.858 / 1.801 / 1.848 ms at 2 / 3 / 4 steps,
+// profiles/r05/ab2)
 constexpr int kK3D = 2;
 #ifndef EKS_K3B_D
-#define EKS_K3B_D 2
+#define EKS_K3B_D 3
 #endif
 constexpr int kK3BD = EKS_K3B_D;
+// algo 3's chains: every unit publishes its aggregate (k3_fwd: its element,
+// k3_bwd: its map) as soon as it has it, before looking at its neighbour, so
+// a later unit never waits for an earlier one's own chain wait -- only for
+// its stream to end (0: only a unit that finds its neighbour not ready
+// publishes one, round 4's rule)
+#ifndef EKS_EAGER_AGG
+#define EKS_EAGER_AGG 0
+#endif
+constexpr bool kEagerAgg = EKS_EAGER_AGG != 0;
+// k3_bwd's look-back instantiation for every batch of the single-view shape
+// (0: only for batches of at most kLbGroups groups, round 4's rule)
+#ifndef EKS_A3_LB_ALL
+#define EKS_A3_LB_ALL 0
+#endif
+constexpr bool kLbAll = EKS_A3_LB_ALL != 0;
+
+// algo 3's chains: wave 0 issues the poll of its neighbour's flag as soon as
+// its own stream ends (before the unit's element / map composition and its
+// barrier), and uses the word at the chain point when it already says
+// "published" -- one load round trip off the chain (0: poll at the chain point)
+#ifndef EKS_EARLY_POLL
+#define EKS_EARLY_POLL 1
+#endif
+constexpr bool kEarlyPoll = EKS_EARLY_POLL != 0;
+
 // k3_bwd's whole-chunk loop: a scheduling barrier after every step (one
 // step's registers live at a time); A/B with -DEKS_K3B_SCHED=0
 #ifndef EKS_K3B_SCHED

@@ -584,6 +584,10 @@ EKS_DEV unsigned k3_fwd_run(const SmoothArgs &a, const Plan3 &p, const Sched3 &s
         stream_steps<LF, D, N>(src, s0, e0, md.off, absorb_el);
       }
     }
+    // wave 0: the neighbour's flag polled now, read at the chain point (the
+    // load flies during the element stores, the barrier and the compositions)
+    unsigned early = 0u;
+    if (kEarlyPoll && w == 0 && cu > 0) early = ld_flag(flags + grp * p.NCu + cu - 1);
     if (!lane_ok) {  // a dead lane's chain stays exact (identity elements)
       El.set_identity();
       if constexpr (FPW > 1) El.store(&shA[w][0][l], 64);
@@ -651,8 +655,18 @@ EKS_DEV unsigned k3_fwd_run(const SmoothArgs &a, const Plan3 &p, const Sched3 &s
       if (cu > 0) {
         const unsigned *fl = flags + grp * p.NCu;  // group-major: a walk reads consecutive words
         long long j = cu - 1;
-        if (!inc_ready(fl + j, a.wait_ticks)) {
-          if (cu + 1 < p.NCu) {
+        const bool agg = cu + 1 < p.NCu;  // (the last unit has no successor)
+        if (kEagerAgg) {
+          // the aggregate's stores go out with the neighbour's poll (the poll's
+          // wait covers them), then its flag: later units fold it instead of
+          // waiting for this unit's own chain wait
+          if (agg && lane_ok) elem_store_pl_wt<R>(Ec, agg1, cu * EL, B, b);
+          const bool ready = inc_ready(fl + j, a.wait_ticks);
+          if (agg) publish_flag(flags + grp * p.NCu + cu, l, kAggReady);
+          if (!ready) j = look_back(fl, j, 1, -1, p.NCu, a.wait_ticks, ok);
+        } else if (!(kEarlyPoll && inc_ready_early(early, a.wait_ticks)) &&
+                   !inc_ready(fl + j, a.wait_ticks)) {
+          if (agg) {
             if (lane_ok) elem_store_pl_wt<R>(Ec, agg1, cu * EL, B, b);
             publish_flag(flags + grp * p.NCu + cu, l, kAggReady);
           }
@@ -927,6 +941,9 @@ EKS_DEV unsigned k3_bwd_run(const SmoothArgs &a, const Plan3 &p, const Sched3 &s
       }
     }
     EKS_STAMP(1, 2);
+    // wave 0: the next unit's flag polled now, read at the chain point
+    unsigned early = 0u;
+    if (kEarlyPoll && w == 0 && cc + 1 < p.NCc) early = ld_flag(flags + grp * p.NCc + cc + 1);
     if (w >= 1) {
       int k = 0;
 #pragma unroll
@@ -977,18 +994,28 @@ EKS_DEV unsigned k3_bwd_run(const SmoothArgs &a, const Plan3 &p, const Sched3 &s
       if (cc + 1 < p.NCc) {
         const unsigned *fl = flags + grp * p.NCc;  // group-major
         long long j = cc + 1;
+        auto store_agg = [&]() {
+          if (lane_ok) {
+#pragma unroll
+            for (int u = 0; u < R; ++u) {
+#pragma unroll
+              for (int q = 0; q < R; ++q) st_wt(&pl(agg2, cc * MP + u * R + q, B, b), UG[u][q]);
+              st_wt(&pl(agg2, cc * MP + R * R + u, B, b), Ug[u]);
+            }
+          }
+        };
+        const bool early_ok = kEarlyPoll && inc_ready_early(early, a.wait_ticks);
         if (!LB) {
-          if (!wait_flag(fl + j, a.wait_ticks, kIncReady)) okc = false;
+          if (!early_ok && !wait_flag(fl + j, a.wait_ticks, kIncReady)) okc = false;
+        } else if (early_ok) {
+        } else if (kEagerAgg) {  // (as k3_fwd: U published with the poll)
+          if (cc > 0) store_agg();
+          const bool ready = inc_ready(fl + j, a.wait_ticks);
+          if (cc > 0) publish_flag(flags + grp * p.NCc + cc, l, kAggReady);
+          if (!ready) j = look_back(fl, j, 1, +1, p.NCc, a.wait_ticks, okc);
         } else if (!inc_ready(fl + j, a.wait_ticks)) {
           if (cc > 0) {
-            if (lane_ok) {
-#pragma unroll
-              for (int u = 0; u < R; ++u) {
-#pragma unroll
-                for (int q = 0; q < R; ++q) st_wt(&pl(agg2, cc * MP + u * R + q, B, b), UG[u][q]);
-                st_wt(&pl(agg2, cc * MP + R * R + u, B, b), Ug[u]);
-              }
-            }
+            store_agg();
             publish_flag(flags + grp * p.NCc + cc, l, kAggReady);
           }
           j = look_back(fl, j, 1, +1, p.NCc, a.wait_ticks, okc);
@@ -1193,7 +1220,7 @@ constexpr long long kLbGroups = 48;
 inline bool a3_bwd_lookback(const Plan3 &p) {
   if (g_a3_lb == 1) return false;
   if (g_a3_lb == 2) return true;
-  return p.ng <= kLbGroups;
+  return kLbAll || p.ng <= kLbGroups;
 }
 
 // host: the launches of one algo-3 call
