@@ -148,6 +148,17 @@ def cpu_cores() -> int:
     return max(1, n)
 
 
+def cpu_cores_cap() -> str:
+    """Why ``cores`` can be below ``host_cpus``: the box's CPU share."""
+    n = len(os.sched_getaffinity(0))
+    for var in ("EKS_CPU_CORES", "OMP_NUM_THREADS"):
+        cap = os.environ.get(var)
+        if cap and cap.isdigit() and 0 < int(cap) < n:
+            return (f"{var}={cap}: this job's CPU share on the box (the affinity mask shows "
+                    f"{n} host CPUs shared with other jobs)")
+    return "the affinity mask"
+
+
 def _cpu_model(O, task):
     """Untimed model fit of one task, from its own ensemble."""
     kind, stack, args = task
@@ -767,7 +778,8 @@ def main():
                            f"(numpy oracle: ensemble + filtering_pass + smooth_backward + "
                            f"projection; model fit untimed), {wall:.1f} s wall; 1-core figure "
                            f"on {one_desc}, {t_hot1:.1f} s"),
-                   host_cpus=len(os.sched_getaffinity(0)))
+                   host_cpus=len(os.sched_getaffinity(0)),
+                   cores_cap=cpu_cores_cap())
 
     if rank == 0:
         backend = None

@@ -40,6 +40,7 @@
 
 #include <cmath>
 #include <cstdint>
+#include <type_traits>
 #include <utility>
 
 #include "../../include/eks_hip.h"
@@ -363,9 +364,6 @@ EKS_DEV K block_select(const K *keys, long long n, long long k, int top,
 constexpr int kCand = 3072;        // LDS candidates (24 KB + 6 KB of indices)
 constexpr int kSelDigit = 8;       // digits of the in-LDS select (1 KB histogram)
 constexpr long long kLdsMaskT = 65536;  // rows with 16-bit frame indices
-// keys per thread of the register-resident selection (256 threads: rows up
-// to 10 240 frames, config 4's 10 000)
-constexpr int kSelKPT = 40;
 
 // KPT > 0 (rows of at most BLK * KPT frames): the row is read ONCE, into
 // KPT registers per thread, and both passes (histogram, compaction + mask)
@@ -1628,72 +1626,62 @@ __global__ __launch_bounds__(256) void k_fitw_accum(const T *__restrict__ obs, F
     }
 }
 
-// k_fit_final's PCA model for n = 10..16 (even): ONE WAVE per trajectory,
-// lane L owning entries (i, j0 .. j0 + 3) of the n x n matrix, i = L / 4,
-// j0 = 4 (L % 4); the round-robin Jacobi's cross-entry reads go through LDS
-// (a one-wave workgroup: its barriers are free).  Round 4's form used 256
-// threads (one entry each) and 4-wave barriers twice per rotation round,
-// ~90 us at 6 cameras for 17 trajectories, bound by those barriers.  The
-// rotation arithmetic per entry is unchanged; the sweep's convergence sums
-// add the same squares in another order.
-constexpr int kFwEnt = kNW * kNW / 64;  // entries per lane
+// k_fit_final's PCA model for n = 10..16 (even): one 256-thread block per
+// trajectory, thread (i, j) = (L / 16, L % 16) owning entry (i, j); the
+// round-robin Jacobi's cross-entry reads go through LDS
 template <int R>
-__global__ __launch_bounds__(64) void k_fitw_final(long long B, const double *__restrict__ part,
-                                                   FitShift ks, int n, double smooth_param,
-                                                   double *__restrict__ params,
-                                                   int32_t *__restrict__ status) {
+__global__ __launch_bounds__(256) void k_fitw_final(long long B, const double *__restrict__ part,
+                                                    FitShift ks, int n, double smooth_param,
+                                                    double *__restrict__ params,
+                                                    int32_t *__restrict__ status) {
   __shared__ double sA[kNW * kNW], sV[kNW * kNW], sM[kNW * kNW], sD[kNW * kNW], sEv[kNW];
+  __shared__ double sRed[2][4];
   const CsRt CS(n);
   const long long b = blockIdx.x;
-  const int L = threadIdx.x, i = L / (kNW / kFwEnt), j0 = (L % (kNW / kFwEnt)) * kFwEnt;
+  const int L = threadIdx.x, i = L / kNW, j = L % kNW;
+  const bool own = i < n && j < n;
   const double *o = part + b * CS.kLen;
   const double cnt = o[CS.cnt];
   double np_ = o[CS.npair];
   if (np_ < 1.0) np_ = __builtin_nan("");
-  double a[kFwEnt], v[kFwEnt], Mij[kFwEnt], Dij[kFwEnt];
-  bool own[kFwEnt];
-#pragma unroll
-  for (int u = 0; u < kFwEnt; ++u) {
-    const int j = j0 + u;
-    own[u] = i < n && j < n;
-    const int ti = own[u] ? (i <= j ? CS.tri(i, j) : CS.tri(j, i)) : 0;
-    const double s1i = own[u] ? o[CS.mean + i] : 0.0, s1j = own[u] ? o[CS.mean + j] : 0.0;
-    const double d1i = own[u] ? o[CS.dmean + i] : 0.0, d1j = own[u] ? o[CS.dmean + j] : 0.0;
-    Mij[u] = own[u] ? o[CS.M + ti] - s1i * (s1j / cnt) : 0.0;
-    Dij[u] = own[u] ? o[CS.dM + ti] - d1i * (d1j / np_) : 0.0;
-    a[u] = Mij[u];
-    v[u] = (own[u] && i == j) ? 1.0 : 0.0;
-  }
+  const int ti = own ? (i <= j ? CS.tri(i, j) : CS.tri(j, i)) : 0;
+  const double s1i = own ? o[CS.mean + i] : 0.0, s1j = own ? o[CS.mean + j] : 0.0;
+  const double d1i = own ? o[CS.dmean + i] : 0.0, d1j = own ? o[CS.dmean + j] : 0.0;
+  const double Mij = own ? o[CS.M + ti] - s1i * (s1j / cnt) : 0.0;
+  const double Dij = own ? o[CS.dM + ti] - d1i * (d1j / np_) : 0.0;
   // packed row [m0 | S0 | A | Q | C (n x R) | offset (n)]
   const int pS0 = R, pA = R + R * R, pQ = R + 2 * R * R, pC = R + 3 * R * R, pOff = pC + n * R;
   double *pr = params + b * (long long)(pOff + n);
   if (L < R) pr[L] = 0.0;
   if (L < R * R) pr[pA + L] = (L / R == L % R) ? 1.0 : 0.0;
   if (L < n) pr[pOff + L] = ks.K[b * n + L] + o[CS.mean + L] / cnt;
+  double a = Mij, v = (own && i == j) ? 1.0 : 0.0;
   const int Nm = n - 1;
   auto slot_of = [&](int x, int k) { return x == 0 ? 0 : 1 + (x - 1 + Nm - (k % Nm)) % Nm; };
   auto idx_at = [&](int pos, int k) { return pos == 0 ? 0 : 1 + (pos - 1 + k) % Nm; };
   for (int sweep = 0; sweep < 60; ++sweep) {
-    double off = 0.0, dia = 0.0;
-#pragma unroll
-    for (int u = 0; u < kFwEnt; ++u) {
-      off += (own[u] && i < j0 + u) ? a[u] * a[u] : 0.0;
-      dia += (own[u] && i == j0 + u) ? a[u] * a[u] : 0.0;
-    }
+    double off = (own && i < j) ? a * a : 0.0, dia = (own && i == j) ? a * a : 0.0;
 #pragma unroll
     for (int w = 32; w >= 1; w >>= 1) {
       off += __shfl_xor(off, w, 64);
       dia += __shfl_xor(dia, w, 64);
     }
-    if (off == 0.0 || off <= 1e-34 * dia) break;  // wave-uniform
+    if ((L & 63) == 0) {
+      sRed[0][L >> 6] = off;
+      sRed[1][L >> 6] = dia;
+    }
+    __syncthreads();
+    off = sRed[0][0] + sRed[0][1] + sRed[0][2] + sRed[0][3];
+    dia = sRed[1][0] + sRed[1][1] + sRed[1][2] + sRed[1][3];
+    __syncthreads();
+    if (off == 0.0 || off <= 1e-34 * dia) break;  // block-uniform
     for (int k = 0; k < Nm; ++k) {
-#pragma unroll
-      for (int u = 0; u < kFwEnt; ++u) {
-        sA[i * kNW + j0 + u] = a[u];
-        sV[i * kNW + j0 + u] = v[u];
-      }
+      sA[L] = a;
+      sV[L] = v;
       __syncthreads();
       auto partner = [&](int x) { return idx_at(Nm - slot_of(x, k), k); };
+      const int li = own ? i : 0, lj = own ? j : 0;
+      const int pi = partner(li), pj = partner(lj);
       auto rot = [&](int x, int px, double &jxx, double &jpx) {
         const int p = x < px ? x : px, q = x < px ? px : x;
         const double apq = sA[p * kNW + q], app = sA[p * kNW + p], aqq = sA[q * kNW + q];
@@ -1707,38 +1695,24 @@ __global__ __launch_bounds__(64) void k_fitw_final(long long B, const double *__
         jxx = cs;
         jpx = x == p ? -sn : sn;
       };
-      const int li = i < n ? i : 0, pi = partner(li);
-      double ji, jpi_i;
+      double ji, jpi_i, jj, jpj_j;
       rot(li, pi, ji, jpi_i);
-      double na[kFwEnt], nv[kFwEnt];
-#pragma unroll
-      for (int u = 0; u < kFwEnt; ++u) {
-        const int lj = own[u] ? j0 + u : 0, pj = partner(lj);
-        double jj, jpj_j;
-        rot(lj, pj, jj, jpj_j);
-        const double a_ipj = sA[li * kNW + pj], a_pij = sA[pi * kNW + lj];
-        const double a_pipj = sA[pi * kNW + pj], v_ipj = sV[li * kNW + pj];
-        const double r0 = a[u] * jj + a_ipj * jpj_j;
-        const double r1 = a_pij * jj + a_pipj * jpj_j;
-        na[u] = own[u] ? ji * r0 + jpi_i * r1 : a[u];
-        nv[u] = own[u] ? v[u] * jj + v_ipj * jpj_j : v[u];
-      }
+      rot(lj, pj, jj, jpj_j);
+      const double a_ipj = sA[li * kNW + pj], a_pij = sA[pi * kNW + lj];
+      const double a_pipj = sA[pi * kNW + pj], v_ipj = sV[li * kNW + pj];
       __syncthreads();
-#pragma unroll
-      for (int u = 0; u < kFwEnt; ++u) {
-        a[u] = na[u];
-        v[u] = nv[u];
+      if (own) {
+        const double r0 = a * jj + a_ipj * jpj_j;
+        const double r1 = a_pij * jj + a_pipj * jpj_j;
+        a = ji * r0 + jpi_i * r1;
+        v = v * jj + v_ipj * jpj_j;
       }
     }
   }
-#pragma unroll
-  for (int u = 0; u < kFwEnt; ++u) {
-    const int e = i * kNW + j0 + u;
-    sV[e] = v[u];
-    sM[e] = Mij[u];
-    sD[e] = Dij[u];
-    if (own[u] && i == j0 + u) sEv[i] = a[u];
-  }
+  sV[L] = v;
+  sM[L] = Mij;
+  sD[L] = Dij;
+  if (own && i == j) sEv[i] = a;
   __syncthreads();
   int order[R];
   unsigned used = 0;
@@ -1768,15 +1742,11 @@ __global__ __launch_bounds__(64) void k_fitw_final(long long B, const double *__
     pr[pS0 + L] = k == l ? s0 / cnt : 0.0;
     pr[pQ + L] = smooth_param * (q / (np_ - 1.0));
   }
+  if (own && j < R) {
+    int oj = 0;
 #pragma unroll
-  for (int u = 0; u < kFwEnt; ++u) {
-    const int j = j0 + u;
-    if (own[u] && j < R) {
-      int oj = 0;
-#pragma unroll
-      for (int w = 0; w < R; ++w) oj = w == j ? order[w] : oj;
-      pr[pC + i * R + j] = sV[i * kNW + oj];
-    }
+    for (int u = 0; u < R; ++u) oj = u == j ? order[u] : oj;
+    pr[pC + i * R + j] = sV[i * kNW + oj];
   }
   if (status && L == 0) status[b] = cnt > 0.0 ? 0 : EKS_STATUS_SINGULAR;
 }
@@ -1933,9 +1903,6 @@ extern "C" int eks_fit(const void *obs, int obs_dtype, int64_t B, int64_t T, int
     } else if (T <= 256 * 16) {  // the row read once, into registers
       hipLaunchKernelGGL((k_fit_select<256, 16>), dim3((unsigned)B), dim3(256), 0, s, worst, T, lo,
                          hi, g, thr, yev ? kept : nullptr, W);
-    } else if (T <= 256 * kSelKPT) {
-      hipLaunchKernelGGL((k_fit_select<256, kSelKPT>), dim3((unsigned)B), dim3(256), 0, s, worst, T,
-                         lo, hi, g, thr, yev ? kept : nullptr, W);
     } else {
       hipLaunchKernelGGL(k_fit_select<256>, dim3((unsigned)B), dim3(256), 0, s, worst, T, lo,
                          hi, g, thr, yev ? kept : nullptr, W);
@@ -1996,7 +1963,7 @@ extern "C" int eks_fit(const void *obs, int obs_dtype, int64_t B, int64_t T, int
       double *src = merge(ic<0>{}, npart);
       if (!src) return EKS_ERR_HIP;
       prof_mark(s, "k_fitw_final");
-      hipLaunchKernelGGL((k_fitw_final<3>), dim3((unsigned)B), dim3(64), 0, s, B, src, ks, n,
+      hipLaunchKernelGGL((k_fitw_final<3>), dim3((unsigned)B), dim3(256), 0, s, B, src, ks, n,
                          smooth_param, params, status);
       prof_call_end(s);
       return check_launch("k_fitw_final");
@@ -2041,8 +2008,12 @@ extern "C" int eks_fit(const void *obs, int obs_dtype, int64_t B, int64_t T, int
         auto accum = [&](auto from_yev, auto wm) {
           constexpr bool FY = decltype(from_yev)::value != 0, WM = decltype(wm)::value != 0;
           const long long lanes = WM ? B * (long long)npart * 64 : B * (long long)sh.NC;
-          hipLaunchKernelGGL((k_fit_accum<EE, NN, Tp, YT, FY, WM>), dim3(grid_for(lanes, 256)),
-                             dim3(256), 0, s, (const Tp *)obs, sh, sb, st, se, sj, E, median, thr,
+          // the plane path never reads the members: one instantiation per (n,
+          // y type), not per member count and type
+          constexpr int EA = FY ? 0 : EE;
+          using TA = typename std::conditional<FY, float, Tp>::type;
+          hipLaunchKernelGGL((k_fit_accum<EA, NN, TA, YT, FY, WM>), dim3(grid_for(lanes, 256)),
+                             dim3(256), 0, s, (const TA *)obs, sh, sb, st, se, sj, E, median, thr,
                              kept, W, partA, yo, ks);
         };
         if (yev) {

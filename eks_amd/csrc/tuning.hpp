@@ -32,6 +32,13 @@ constexpr int kK3D = 2;
 #define EKS_K3B_D 3
 #endif
 constexpr int kK3BD = EKS_K3B_D;
+// the same from the fit's y / ev hand-off planes (f32 y, f64 ev: 24 B per
+// step and lane instead of 40): a deeper ring keeps the bytes in flight
+#ifndef EKS_K3_YEV_D
+#define EKS_K3_YEV_D 4
+#endif
+constexpr int kK3YevD = EKS_K3_YEV_D;
+
 // algo 3's chains: every unit publishes its aggregate (k3_fwd: its element,
 // k3_bwd: its map) as soon as it has it, before looking at its neighbour, so
 // a later unit never waits for an earlier one's own chain wait -- only for

@@ -469,7 +469,7 @@ template <int R, int N, int E, typename T, int AI, int CI>
 EKS_DEV unsigned k3_fwd_run(const SmoothArgs &a, const Plan3 &p, const Sched3 &sc, unsigned t,
                             double *lds, unsigned *tk, unsigned *ctr, int &it) {
   constexpr int EL = Elem<R>::len, KS = R + Sym<R>::len;
-  constexpr int D = kK3D;
+  constexpr int D = is_yev<T>::value ? kK3YevD : kK3D;
   constexpr int LF = fine_len3(R, N);
   constexpr int FPW = fwd_fpw<R>(), KPU = kWV * FPW;
   constexpr int NA = FPW > 1 ? kWV : 1;
@@ -793,7 +793,7 @@ template <int R, int N, int E, typename T, int AI, int CI, bool NLL, bool LB>
 EKS_DEV unsigned k3_bwd_run(const SmoothArgs &a, const Plan3 &p, const Sched3 &sc, unsigned t,
                             double *lds, unsigned *tk, unsigned *ctr, int &it) {
   constexpr int KS = R + Sym<R>::len, MP = R * R + R;
-  constexpr int D = kK3BD;
+  constexpr int D = is_yev<T>::value ? kK3YevD : kK3BD;
   constexpr int NR = reg_steps3(R, N), NL = lds_steps3(R, N), LF = NR + NL;
   auto &fs = *reinterpret_cast<double (*)[NL][KS][64 * kWV]>(lds);  // filtered states, first NL steps
   auto &shM = *reinterpret_cast<double (*)[kWV - 1][MP][64]>(lds + NL * KS * 64 * kWV);  // maps of waves 1..3
