@@ -642,12 +642,16 @@ EKS_DEV void load_model_pl(const double *base, long long B, unsigned b, bool wit
   for (int i = 0; i < N; ++i) md.off[i] = pl(base, L::off + i, B, b);
 }
 
-// one thread per trajectory: params rows -> planes, model structure check
+// one thread per trajectory: params rows -> planes, model structure check;
+// and the call's chain sync block (tickets, flags: `zw` 16-byte words) zeroed
+// on the way, so a graph step has no memset node in front of the passes
 template <int R, int N, int AI, int CI>
 __global__ __launch_bounds__(256) void k_model_planes(const double *params, long long B,
-                                                      double *planes, int32_t *status) {
+                                                      double *planes, int32_t *status,
+                                                      uint4 *zero, long long zw) {
   using L = ParamLayout<R, N>;
   const long long b = (long long)blockIdx.x * 256 + threadIdx.x;
+  for (long long i = b; i < zw; i += (long long)gridDim.x * 256) zero[i] = make_uint4(0u, 0u, 0u, 0u);
   if (b >= B) return;
   const double *pp = params + b * L::len;
 #pragma unroll

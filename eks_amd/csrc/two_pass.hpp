@@ -1235,11 +1235,15 @@ int launch_algo3_one(const SmoothArgs &a) {
     int rc;
     prof_call_begin();
     prof_mark(a.stream, "k_model_planes");
-    // tickets and chain flags start at zero every call (graph capture: a memset node)
-    if (hipMemsetAsync(a.ws, 0, p.sync_bytes, a.stream) != hipSuccess)
+    // tickets and chain flags start at zero every call: k_model_planes zeroes
+    // them (sync_bytes is a multiple of 256), or a memset node when the
+    // caller's workspace is not 16-byte aligned
+    const bool zk = ((uintptr_t)a.ws & 15) == 0;
+    if (!zk && hipMemsetAsync(a.ws, 0, p.sync_bytes, a.stream) != hipSuccess)
       return set_err(EKS_ERR_HIP, "eks_smooth algo 3: hipMemsetAsync failed");
     hipLaunchKernelGGL((k_model_planes<R, N, AI, CI>), dim3(grid_for(a.B, 256)), dim3(256), 0, a.stream,
-                       a.params, a.B, (double *)(a.ws + p.prm_off), a.status);
+                       a.params, a.B, (double *)(a.ws + p.prm_off), a.status, (uint4 *)a.ws,
+                       zk ? (long long)(p.sync_bytes / sizeof(uint4)) : 0LL);
     if ((rc = check_launch("k_model_planes"))) return rc;
     // the single-view model: the throughput shape (config 4)
     constexpr bool kSingleView = R == 2 && N == 2 && AI == kAId && CI == kCId;
