@@ -1767,9 +1767,17 @@ void fit_chunks(long long B, long long T, int &nc, long long &lc, int n = 0) {
 
 constexpr int kMergeFan = 16;
 
-// few long trajectories: k_fit_accum merges each wave's 64 chunks itself
-bool fit_wave_merge(int nc, int n = 0) { return n <= kMaxObs && nc >= 64; }
-int fit_partials(int nc, int n = 0) { return fit_wave_merge(nc, n) ? (nc + 63) / 64 : nc; }
+// few long trajectories (B < 64: a trajectory-fastest wave would span
+// several chunks of short row segments): k_fit_accum merges each wave's 64
+// chunks itself.  From 64 trajectories on, the lanes stay trajectory-fastest
+// (one coalesced row segment per frame and wave; the 8-GPU shard of config
+// 4, B = 2 176, nc = 105: the wave-merge form's lanes 96 frames apart in the
+// time-major y plane fetched 1.18 GB for its 0.17 GB) and k_fit_merge
+// reduces the nc partials.
+bool fit_wave_merge(long long B, int nc, int n = 0) { return n <= kMaxObs && nc >= 64 && B < 64; }
+int fit_partials(long long B, int nc, int n = 0) {
+  return fit_wave_merge(B, nc, n) ? (nc + 63) / 64 : nc;
+}
 constexpr int kMaxObsFit = kNW;  // n of eks_fit (even; n > kMaxObs: the wide kernels)
 
 }  // namespace
@@ -1784,7 +1792,7 @@ extern "C" size_t eks_fit_workspace_bytes(int64_t B, int64_t T, int n) {
   long long lc;
   fit_chunks(B, T, nc, lc, n);
   const long long len = 2 + 4LL * n + (long long)n * (n + 1);
-  const long long np = fit_partials(nc, n);
+  const long long np = fit_partials(B, nc, n);
   const long long nc2 = (np + kMergeFan - 1) / kMergeFan;
   const long long W = (T + 63) / 64;  // frame-mask words per trajectory
   // worst plane, thresholds, chunk partials, kept-frame mask, shifts K
@@ -1841,8 +1849,8 @@ extern "C" int eks_fit(const void *obs, int obs_dtype, int64_t B, int64_t T, int
   const long long len = 2 + 4LL * n + (long long)n * (n + 1);
   double *worst = (double *)workspace;
   double *thr = worst + B * T;
-  const int npart = fit_partials(sh.NC, n);
-  const bool wave_merge = fit_wave_merge(sh.NC, n);
+  const int npart = fit_partials(B, sh.NC, n);
+  const bool wave_merge = fit_wave_merge(B, sh.NC, n);
   double *partA = thr + B;
   double *partB = partA + B * (long long)npart * len;
   const long long W = (T + 63) / 64;

@@ -26,8 +26,11 @@ constexpr bool kHandoffFences = EKS_HANDOFF_FENCES != 0;
 
 // member prefetch distance (steps) of both algo-3 passes; k3_bwd its own
 // (config 4, one box: k3_bwd 1.858 / 1.801 / 1.848 ms at 2 / 3 / 4 steps,
-// profiles/r05/ab2)
-constexpr int kK3D = 2;
+// profiles/r05/ab2; k3_fwd 1.397 / 1.408 / 1.412 ms, profiles/r05/ab7)
+#ifndef EKS_K3F_D
+#define EKS_K3F_D 2
+#endif
+constexpr int kK3D = EKS_K3F_D;
 #ifndef EKS_K3B_D
 #define EKS_K3B_D 3
 #endif

@@ -14,7 +14,7 @@ for src in eks_amd/csrc/*.hip eks_amd/csrc/*.cpp; do
   hit=""
   for u in "$@"; do [ "$(basename $u .hip)" = "$b" ] && hit=1; done
   if [ -n "$hit" ]; then
-    /opt/rocm/bin/hipcc $FLAGS -O3 -std=c++17 -fPIC --offload-arch=gfx950 -c $src -o $OUT/obj/$b.o &
+    /opt/rocm/bin/hipcc $FLAGS -O3 -std=c++17 -fPIC --offload-arch=gfx950 --offload-compress -c $src -o $OUT/obj/$b.o &
     OBJS="$OBJS $OUT/obj/$b.o"
   else
     OBJS="$OBJS eks_amd/lib/obj/$b.o"
