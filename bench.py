@@ -671,6 +671,12 @@ def main():
     eager_step = step
     if graph is not None:
         step = graph.replay
+        # the replays warmed right before the timed region as well: the first
+        # steps after the capture's idle gap run ~10 % slow while the GPU
+        # ramps (tools/first_step.py, profiles/r05/ab8), which W = 5 eager
+        # steps before the capture do not cover
+        for _ in range(a.warmup):
+            step()
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -699,15 +705,35 @@ def main():
     e2e = None
     if "fit_step" in w:
         fit_step, e2e_smooth = w["fit_step"], w["e2e_smooth"]
-        for _ in range(max(1, a.warmup)):
+
+        def e2e_eager():
             fit_step()
             e2e_smooth()
+
+        for _ in range(max(1, a.warmup)):
+            e2e_eager()
         torch.cuda.synchronize()
+        # replayed as one HIP graph like the hot-path step (eager: ~15 launches
+        # whose host cost the small configurations would otherwise time)
+        e2e_run = e2e_eager
+        if graph is not None:
+            try:
+                ge = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(ge):
+                    e2e_eager()
+                ge.replay()
+                torch.cuda.synchronize()
+                e2e_run = ge.replay
+                for _ in range(max(1, a.warmup)):
+                    e2e_run()
+            except Exception as exc:  # pragma: no cover - depends on the runtime
+                print(f"[bench] end-to-end graph capture failed ({exc}); launching eagerly",
+                      file=sys.stderr)
         dist.barrier()
+        torch.cuda.synchronize()
         f0 = time.perf_counter()
         for _ in range(a.steps):
-            fit_step()
-            e2e_smooth()
+            e2e_run()
         torch.cuda.synchronize()
         dist.barrier()
         e2e_s = dist.max_over_ranks(time.perf_counter() - f0, device=dev)
@@ -719,6 +745,7 @@ def main():
         fit_kernels = [(n, ms / a.steps) for n, ms in _lib.profile_end()]
         assert_clean(torch, w, "end-to-end kernel-timing loop")
         e2e = dict(value=units_total / e2e_s * a.steps, ms_per_step=e2e_s / a.steps * 1e3,
+                   hip_graph=e2e_run is not e2e_eager,
                    kernels_ms={n: round(ms, 4) for n, ms in fit_kernels},
                    scope="eks_fit (ensemble, good-frame percentile, model fit; writes the "
                          "ensemble planes) + eks_smooth from those planes (members read once)")

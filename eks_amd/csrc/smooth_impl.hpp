@@ -211,6 +211,9 @@ struct ChunkPlan {
   // of one trajectory): y / ev are stored once, as a single plane column
   long long yB = 0;
   EKS_DEV unsigned ylane(unsigned b) const { return yB == 1 ? 0u : b; }
+  // single-column planes (yB = 1) read by waves whose lanes all lie in one
+  // chunk (UNI, or B a multiple of 64): K1 loads them with scalar loads
+  int ywave = 0;
   size_t y_off = 0, ev_off = 0, elem_off = 0, cstart_off = 0, bwd_off = 0, nllp_off = 0,
          msend_off = 0, ckpt_off = 0, total = 0;
   // chained chunk scans (k_c2_fscan_g / k_c4_bscan_g): G blocks per
@@ -674,6 +677,45 @@ EKS_DEV void c1_stream(const SmoothArgs &a, const ChunkPlan &p, long long s, lon
     // a cache-hit re-read), so they stay in flight: a load under a
     // lane-divergent `if` is merged into its slot by a copy that waits for it
     constexpr int DY = 2;
+    if (p.ywave) {
+      // every lane of the wave reads the same step of the single-column
+      // planes (members shared by all trajectories, e.g. the pupil sweep's
+      // candidate models): scalar loads into SGPRs through the constant
+      // address space, so the ring costs no VGPRs (K1 of the sweep is bound
+      // by its FP64 chains at the waves per SIMD its VGPRs allow)
+      using CY = const __attribute__((address_space(4))) YT;
+      using CE = const __attribute__((address_space(4))) double;
+      CY *yp = (CY *)p.ysrc;
+      CE *ep = (CE *)p.evsrc;
+      const int su = __builtin_amdgcn_readfirstlane((int)s);
+      const int eu = __builtin_amdgcn_readfirstlane((int)e);
+      YT ys[DY][N];
+      double es[DY][N];
+      auto sfetch = [&](int q, int t) {
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+          ys[q][j] = yp[t * N + j];
+          es[q][j] = ep[t * N + j];
+        }
+      };
+#pragma unroll
+      for (int q = 0; q < DY; ++q) sfetch(q, min(su + q, eu - 1));
+      for (int t0 = su; t0 < eu; t0 += DY) {
+#pragma unroll
+        for (int q = 0; q < DY; ++q) {
+          const int t = t0 + q;
+          double y[N], rv[N];
+#pragma unroll
+          for (int j = 0; j < N; ++j) {
+            y[j] = (double)ys[q][j] - off[j];
+            rv[j] = es[q][j];
+          }
+          sfetch(q, min(t + DY, eu - 1));
+          if (t < eu) absorb((long long)t, y, rv);
+        }
+      }
+      return;
+    }
     YT yr[DY][N];
     double er[DY][N];
     auto fetch = [&](int q, long long t) {
@@ -904,8 +946,13 @@ EKS_DEV void c1_elem_body(const SmoothArgs &a, const ChunkPlan &p) {
   }
 }
 
+// EKS_C1_WAVES: k_c1_elem's waves per SIMD asked of the register allocator
+// for the pupil shape (tuning experiments; 0: the compiler's choice)
+#ifndef EKS_C1_WAVES
+#define EKS_C1_WAVES 0
+#endif
 template <int R, int N, int E, typename T, typename YT, int AI, int CI, bool UNI>
-__global__ __launch_bounds__(kBlock) void k_c1_elem(SmoothArgs a, ChunkPlan p) {
+__global__ __launch_bounds__(kBlock, (CI == kCPupil && EKS_C1_WAVES > 0) ? EKS_C1_WAVES : 1) void k_c1_elem(SmoothArgs a, ChunkPlan p) {
   c1_elem_body<R, N, E, T, YT, AI, CI, UNI>(a, p);
 }
 
@@ -2103,6 +2150,8 @@ int launch_shape(const SmoothArgs &a, int algo, long long L) {
   p.nll_fused = (p.nll_closed && p.NC > wave_scan_chunks()) ? 1 : 0;
   const bool shared = !yev && a.sb == 0 && a.B > 1;
   p.yB = shared ? 1 : a.B;
+  // (int step indices in the scalar path: T < 2^31 / N)
+  p.ywave = (shared && (uniform_lanes(a.B) || a.B % 64 == 0) && a.T * N < (1LL << 31)) ? 1 : 0;
   const bool uni = uniform_lanes(a.B);
   // group mode: few trajectories, smoothing, whole pipeline, chained scans
   // (B <= 256: every block but the last holds chunks of every trajectory)

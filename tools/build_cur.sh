@@ -4,6 +4,17 @@
 # (eks_amd/lib/obj) for the others -> exp/NAME/libeks_hip.so (EKS_LIB=...).
 #   tools/build_cur.sh NAME [-DFLAG ...] unit1.hip [unit2.hip ...]
 set -e
+# The other units come from the last full build: a header changed since then
+# (a struct layout, an inline function) would mix two definitions of the same
+# weak symbols in one library (ChunkPlan / make_plan: a GPU memory fault in
+# round 5).  Refuse; run python -m eks_amd.build first.
+oldest=$(ls -tr eks_amd/lib/obj/*.o | head -n 1)
+for h in eks_amd/csrc/*.hpp include/*.h; do
+  if [ "$h" -nt "$oldest" ]; then
+    echo "build_cur.sh: $h is newer than the last full build ($oldest): rebuild first" >&2
+    exit 2
+  fi
+done
 NAME=$1; shift
 FLAGS=""; while [[ "$1" == -* ]]; do FLAGS="$FLAGS $1"; shift; done
 OUT=exp/$NAME; rm -rf $OUT; mkdir -p $OUT/obj
