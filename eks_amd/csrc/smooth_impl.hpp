@@ -290,11 +290,18 @@ inline ChunkPlan make_plan(long long B, long long T, int r, int n, long long L,
   if (p.NC > wave_scan_chunks()) {
     // blocks per trajectory: few lanes in all -> ~1 chunk per thread (the
     // scan is latency bound); many -> q chunks per thread so the chip holds
-    // ~4 blocks per CU (the Hillis-Steele trees cost ~6 compositions per
-    // lane, the per-thread runs 1 per chunk: config 5's 64 x 17 858 chunks).
-    // At most 64 blocks: their totals are combined by one wave.
+    // ~2 blocks per CU (the Hillis-Steele trees cost ~6 compositions per
+    // lane, the per-thread runs 1 per chunk: config 5's 64 x 17 858 chunks,
+    // q = 2 / 4 / 8 / 16: K2 0.238 / 0.188 / 0.175 / 0.194 ms,
+    // profiles/r05/ab9).  At most 64 blocks: their totals are combined by
+    // one wave.
+    static const long long qt_force = [] {  // EKS_SCAN_QT: tuning experiments only
+      const char *e = getenv("EKS_SCAN_QT");
+      return e ? atoll(e) : 0LL;
+    }();
     auto blocks = [&](long long nc, int &G, long long &cpb) {
-      const long long qt = std::min<long long>(8, std::max<long long>(1, B * nc / (256LL * 256 * 4)));
+      const long long qt = qt_force > 0 ? qt_force
+                                        : std::min<long long>(8, std::max<long long>(1, B * nc / (256LL * 256 * 2)));
       G = (int)std::min<long long>(64, std::max<long long>(1, (nc + 256 * qt - 1) / (256 * qt)));
       cpb = (nc + G - 1) / G;
     };
@@ -792,19 +799,48 @@ EKS_DEV void c1_stream(const SmoothArgs &a, const ChunkPlan &p, long long s, lon
 template <int E, int N, typename T, typename YT>
 __global__ __launch_bounds__(kBlock) void k_c0_shared(SmoothArgs a, ChunkPlan p) {
   const long long t = blockIdx.x * (long long)kBlock + threadIdx.x;
-  if (t >= a.T) return;
   constexpr int EE = E > 0 ? E : 1;
   const T *pt = (const T *)a.obs + t * a.st;
   T cur[EE][N];
   // a step's E x N members contiguous and 16-byte aligned (the pupil sweep's
   // (T, E, 8) float32 layout): 16-byte loads, a quarter of the requests
   constexpr bool kVec = E > 0 && (E * N) % 4 == 0 && std::is_same<T, float>::value;
+  constexpr int Q = kVec ? EE * N / 4 : 1;  // 16-byte words per step
   const bool vec = kVec && a.sj == 1 && a.se == N && (((uintptr_t)a.obs | (uintptr_t)(a.st * 4)) & 15) == 0;
+  // consecutive steps contiguous too: the block's 256 steps are one run of
+  // 256 Q words, loaded word-per-lane (every wave instruction one contiguous
+  // 1 KB) and handed to the step lanes through LDS -- a lane reading its own
+  // step's Q words directly puts 64 lanes 16 Q bytes apart on every load
+  // (config 5: 160 MB of members at ~1.7 TB/s)
+  __shared__ float4 stage[kVec ? kBlock * Q : 1];
+  const bool staged = vec && a.st == (long long)E * N;
+  if constexpr (kVec) {
+    if (staged) {
+      const long long tb = blockIdx.x * (long long)kBlock;
+      const int nq = (int)(min((long long)kBlock, a.T - tb) * Q);
+      const float4 *src = reinterpret_cast<const float4 *>((const float *)a.obs + tb * a.st);
+      float4 r[Q];
+#pragma unroll
+      for (int k = 0; k < Q; ++k) {
+        const int i = threadIdx.x + k * kBlock;
+        r[k] = i < nq ? src[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int k = 0; k < Q; ++k) stage[threadIdx.x + k * kBlock] = r[k];
+      __syncthreads();
+    }
+  }
+  if (t >= a.T) return;
   if constexpr (kVec) {
     if (vec) {
       float4 q[EE * N / 4];
+      if (staged) {
 #pragma unroll
-      for (int k = 0; k < EE * N / 4; ++k) q[k] = reinterpret_cast<const float4 *>(pt)[k];
+        for (int k = 0; k < EE * N / 4; ++k) q[k] = stage[threadIdx.x * Q + k];
+      } else {
+#pragma unroll
+        for (int k = 0; k < EE * N / 4; ++k) q[k] = reinterpret_cast<const float4 *>(pt)[k];
+      }
 #pragma unroll
       for (int k = 0; k < EE * N / 4; ++k) {
         const float w[4] = {q[k].x, q[k].y, q[k].z, q[k].w};
@@ -946,13 +982,8 @@ EKS_DEV void c1_elem_body(const SmoothArgs &a, const ChunkPlan &p) {
   }
 }
 
-// EKS_C1_WAVES: k_c1_elem's waves per SIMD asked of the register allocator
-// for the pupil shape (tuning experiments; 0: the compiler's choice)
-#ifndef EKS_C1_WAVES
-#define EKS_C1_WAVES 0
-#endif
 template <int R, int N, int E, typename T, typename YT, int AI, int CI, bool UNI>
-__global__ __launch_bounds__(kBlock, (CI == kCPupil && EKS_C1_WAVES > 0) ? EKS_C1_WAVES : 1) void k_c1_elem(SmoothArgs a, ChunkPlan p) {
+__global__ __launch_bounds__(kBlock) void k_c1_elem(SmoothArgs a, ChunkPlan p) {
   c1_elem_body<R, N, E, T, YT, AI, CI, UNI>(a, p);
 }
 
