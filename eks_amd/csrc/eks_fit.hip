@@ -263,6 +263,47 @@ EKS_DEV void for_keys(const K *keys, long long n, F &&f) {
   for (; i < n; i += BLK) f(keys[i], i);
 }
 
+// Jacobi rotation (c, s) of the pair p < q that zeroes a_pq:
+//   t = sgn(theta) / (|theta| + sqrt(theta^2 + 1)), theta = (a_qq - a_pp) / (2 a_pq)
+//     = sgn(theta) |h| / (|d| + sqrt(d^2 + h^2)),  d = a_qq - a_pp, h = 2 a_pq,
+//   c = 1 / sqrt(t^2 + 1), s = t c,
+// from the hardware reciprocal / reciprocal square root plus Newton steps
+// (~22 dependent VALU ops; the IEEE form's three divisions and two square
+// roots were ~700 cycles per round of the PCA's Jacobi -- k_fitw_final
+// 0.100 ms at 6 cameras).  The rotation is exact to a few ulp; Jacobi's
+// convergence does not depend on it.
+EKS_DEV double nr_rcp(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  double e = fma(-x, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-x, r, 1.0);
+  return fma(r, e, r);
+}
+EKS_DEV double nr_rsq(double x) {  // x > 0
+  double y = __builtin_amdgcn_rsq(x);
+  double hx = 0.5 * x;
+  y = y * fma(-hx * y, y, 1.5);
+  return y * fma(-hx * y, y, 1.5);
+}
+// the PCA Jacobi's convergence bound on (off-diagonal / diagonal) squared
+// mass: 1e-30 ~ n eps^2, the level rounding leaves (round 4: 1e-34)
+#ifndef EKS_JACOBI_TOL
+#define EKS_JACOBI_TOL 1e-30
+#endif
+constexpr double kJacobiTol = EKS_JACOBI_TOL;
+EKS_DEV void jacobi_cs(double app, double aqq, double apq, double &c, double &s) {
+  c = 1.0;
+  s = 0.0;
+  if (apq == 0.0) return;
+  const double d = aqq - app, h = 2.0 * apq;
+  const double x = fma(d, d, h * h);
+  const double r = x * nr_rsq(x);  // sqrt(d^2 + h^2)
+  double t = fabs(h) * nr_rcp(fabs(d) + r);
+  if (d != 0.0 && ((d < 0.0) != (h < 0.0))) t = -t;  // theta < 0
+  c = nr_rsq(fma(t, t, 1.0));
+  s = t * c;
+}
+
 // lane 0 of the wave's active lanes (the writer of a ballot word)
 EKS_DEV bool first_active_lane() {
   return (int)(threadIdx.x & 63) == __ffsll((long long)__ballot(1)) - 1;
@@ -1287,6 +1328,7 @@ __global__ __launch_bounds__(64) void k_fit_final(long long B, const double *__r
     const int Nm = N - 1;
     auto slot_of = [&](int x, int k) { return x == 0 ? 0 : 1 + (x - 1 + Nm - (k % Nm)) % Nm; };
     auto idx_at = [&](int pos, int k) { return pos == 0 ? 0 : 1 + (pos - 1 + k) % Nm; };
+    double off_prev = __builtin_inf();
     for (int sweep = 0; sweep < 60; ++sweep) {
       double off = (own && i < j) ? a * a : 0.0, dia = (own && i == j) ? a * a : 0.0;
 #pragma unroll
@@ -1294,7 +1336,11 @@ __global__ __launch_bounds__(64) void k_fit_final(long long B, const double *__r
         off += __shfl_xor(off, w, 64);
         dia += __shfl_xor(dia, w, 64);
       }
-      if (off == 0.0 || off <= 1e-34 * dia) break;
+      // converged: the off-diagonal mass at the rounding level of the
+      // diagonal, or no longer shrinking (FMA-rounded rotations can leave
+      // it hovering just above a tighter bound for the remaining sweeps)
+      if (off == 0.0 || off <= kJacobiTol * dia || off >= off_prev) break;
+      off_prev = off;
       for (int k = 0; k < Nm; ++k) {
         // the partner of index x in round k: positions pos and N-1-pos pair up
         auto partner = [&](int x) { return idx_at(Nm - slot_of(x, k), k); };
@@ -1305,13 +1351,8 @@ __global__ __launch_bounds__(64) void k_fit_final(long long B, const double *__r
           const int p = x < px ? x : px, q = x < px ? px : x;
           const double apq = __shfl(a, p * N + q, 64);
           const double app = __shfl(a, p * N + p, 64), aqq = __shfl(a, q * N + q, 64);
-          double c = 1.0, sn = 0.0;
-          if (apq != 0.0) {
-            const double theta = (aqq - app) / (2.0 * apq);
-            const double t = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
-            c = 1.0 / sqrt(t * t + 1.0);
-            sn = t * c;
-          }
+          double c, sn;
+          jacobi_cs(app, aqq, apq, c, sn);
           jxx = c;
           jpx = x == p ? -sn : sn;  // J_qp = -s (x = p), J_pq = s (x = q)
         };
@@ -1659,6 +1700,7 @@ __global__ __launch_bounds__(256) void k_fitw_final(long long B, const double *_
   const int Nm = n - 1;
   auto slot_of = [&](int x, int k) { return x == 0 ? 0 : 1 + (x - 1 + Nm - (k % Nm)) % Nm; };
   auto idx_at = [&](int pos, int k) { return pos == 0 ? 0 : 1 + (pos - 1 + k) % Nm; };
+  double off_prev = __builtin_inf();
   for (int sweep = 0; sweep < 60; ++sweep) {
     double off = (own && i < j) ? a * a : 0.0, dia = (own && i == j) ? a * a : 0.0;
 #pragma unroll
@@ -1674,7 +1716,8 @@ __global__ __launch_bounds__(256) void k_fitw_final(long long B, const double *_
     off = sRed[0][0] + sRed[0][1] + sRed[0][2] + sRed[0][3];
     dia = sRed[1][0] + sRed[1][1] + sRed[1][2] + sRed[1][3];
     __syncthreads();
-    if (off == 0.0 || off <= 1e-34 * dia) break;  // block-uniform
+    if (off == 0.0 || off <= kJacobiTol * dia || off >= off_prev) break;  // block-uniform
+    off_prev = off;
     for (int k = 0; k < Nm; ++k) {
       sA[L] = a;
       sV[L] = v;
@@ -1685,13 +1728,8 @@ __global__ __launch_bounds__(256) void k_fitw_final(long long B, const double *_
       auto rot = [&](int x, int px, double &jxx, double &jpx) {
         const int p = x < px ? x : px, q = x < px ? px : x;
         const double apq = sA[p * kNW + q], app = sA[p * kNW + p], aqq = sA[q * kNW + q];
-        double cs = 1.0, sn = 0.0;
-        if (apq != 0.0) {
-          const double theta = (aqq - app) / (2.0 * apq);
-          const double t = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
-          cs = 1.0 / sqrt(t * t + 1.0);
-          sn = t * cs;
-        }
+        double cs, sn;
+        jacobi_cs(app, aqq, apq, cs, sn);
         jxx = cs;
         jpx = x == p ? -sn : sn;
       };

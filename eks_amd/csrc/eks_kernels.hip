@@ -55,7 +55,7 @@ void clear_err() { g_err.clear(); }
 struct Prof {
   bool on = false;
   int max_calls = 0, call = -1, mark = 0;
-  static constexpr int kMarks = 8;
+  static constexpr int kMarks = 16;  // a split-selection fit call has 10-12 marks
   std::vector<hipEvent_t> ev;
   std::vector<int> nmarks;
   std::vector<std::string> names;  // [call * kMarks + mark]: kernel launched after the mark
