@@ -160,7 +160,12 @@ def test_wide_fit_handoff_then_time_parallel_smooth(torch, V, E, dtype):
     obs = torch.from_numpy(np.ascontiguousarray(st.transpose(2, 1, 0, 3))).cuda()  # (K, T, E, n)
     params, _, yev = batch.fit(obs, kind="multicam", n=n, r=3, smooth_param=0.01,
                                quantile_keep=25, keep_yev=True)
-    a = batch.smooth(obs, params, n=n, r=3, want_nll=True, check=True)
-    b = batch.smooth(yev, params, n=n, r=3, want_nll=True, check=True)
+    a = batch.smooth(obs, params, n=n, r=3, algo=4, want_nll=True, check=True)
+    b = batch.smooth(yev, params, n=n, r=3, algo=4, want_nll=True, check=True)
     assert torch.equal(a["out"], b["out"])
     assert torch.equal(a["nll"], b["nll"])
+    # the automatic choice (six cameras: the compiled r = 3, n = 12 kernels,
+    # whose compile-time-E ensemble contracts differently) from the planes
+    c = batch.smooth(yev, params, n=n, r=3, want_nll=True, check=True)
+    assert float((c["out"] - a["out"]).abs().max()) < 1e-8
+    torch.testing.assert_close(c["nll"], a["nll"], rtol=1e-10, atol=0)
