@@ -27,7 +27,7 @@ int pick_algo(long long B, long long T, int n, int r, int E, int algo) {
 }
 
 bool shape_compiled(int r, int n) {
-  return (r == 2 && n == 2) || (r == 3 && (n == 4 || n == 6 || n == 8 || n == 12));
+  return (r == 2 && n == 2) || (r == 3 && (n == 4 || n == 6 || n == 8 || n == 12 || n == 16));
 }
 
 // the runtime-n kernel (one lane per trajectory, any n <= kMaxObsRt): shapes
@@ -133,6 +133,7 @@ static int smooth_call(const void *obs, int obs_dtype, int64_t B, int64_t T, int
   if (n == 4) return launch_34(a, al, L);
   if (n == 6) return launch_36(a, al, L);
   if (n == 12) return launch_312(a, al, L);
+  if (n == 16) return launch_316(a, al, L);
   return launch_38(a, al, L);
 }
 

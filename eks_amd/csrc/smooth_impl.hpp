@@ -2370,5 +2370,6 @@ int launch_34(const SmoothArgs &a, int algo, long long L);
 int launch_36(const SmoothArgs &a, int algo, long long L);
 int launch_38(const SmoothArgs &a, int algo, long long L);
 int launch_312(const SmoothArgs &a, int algo, long long L);
+int launch_316(const SmoothArgs &a, int algo, long long L);
 
 }  // namespace eks

@@ -180,8 +180,8 @@ int64_t eks_param_len(int n, int r);
  *            E in 3..5 or y / ev planes, else algo 2),
  *            4 = the runtime-n kernels (any n <= 64, r = 2 or 3, members or
  *            y / ev planes): what every (r, n) without compiled kernels runs --
- *            (2, 2) and (3, 4|6|8|12) are compiled; e.g. the multi-camera model
- *            with V = 5 or V > 6 cameras, n = 2V (the reference accepts any V:
+ *            (2, 2) and (3, 4|6|8|12|16) are compiled; e.g. the multi-camera model
+ *            with V = 5, 7 or V > 8 cameras, n = 2V (the reference accepts any V:
  *            eks/multiview_pca_smoother.py:641-666).  eks_smooth_algo
  *            reports 4 for those shapes.  Many trajectories: one GPU lane
  *            per trajectory, sequential in time; few long ones: algo 2's
