@@ -102,6 +102,34 @@ def test_pupil_sweep_nll_matches_dense(torch):
         assert abs(got - want) <= 1e-9 * abs(want), (i, got, want)
 
 
+def test_pupil_sweep_64_candidates_scalar_planes(torch):
+    """64 candidates (a multiple of 64: every wave of the sweep's K1 reads one
+    step of the shared y / ev planes, through scalar loads) against the same
+    members handed over per candidate (no sharing: the vector path) and the
+    oracle; the 16-candidate sweep above covers the per-lane loads."""
+    from eks_amd import batch, synthetic
+    from oracle import eks_oracle as O
+    T = 20000
+    st = synthetic.pupil_obs(np.random.default_rng(11), 5, T, a=0.99).astype(np.float64)
+    preds, ev = O.ensemble_array(st)
+    dg = 1.0 - np.geomspace(1e-4, 1e-1, 8)
+    grid = [(dd, c) for dd in dg for c in dg]
+    models = _models([preds] * len(grid), [[dd, c, c] for dd, c in grid])
+    params, flags = _pack(models)
+    obs = torch.from_numpy(st.astype(np.float32)).cuda().permute(1, 0, 2).unsqueeze(0)
+    shared = obs.expand(len(grid), -1, -1, -1)      # batch stride 0
+    copies = shared.contiguous()                    # one copy per candidate
+    for algo in (0, 2):
+        a = batch.nll(shared, params, n=8, r=3, algo=algo, flags=flags).cpu().numpy()
+        b = batch.nll(copies, params, n=8, r=3, algo=algo, flags=flags).cpu().numpy()
+        np.testing.assert_allclose(a, b, rtol=1e-12)
+    pre, evp = O.ensemble_array(st.astype(np.float32).astype(np.float64))
+    for i in (0, 27, 63):
+        m = models[i]
+        want = O.compute_nll(pre - m["offset"], m["m0"], m["S0"], m["C"], m["A"], m["Q"], evp)
+        assert abs(float(a[i]) - want) <= 1e-9 * abs(want), (i, float(a[i]), want)
+
+
 def test_pupil_both_rows_exact_is_singular(torch):
     """Both members of a folded pair observed exactly (zero ensemble variance
     in columns 5 and 7 at one frame): the reference's S has two equal rows

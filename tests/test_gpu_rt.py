@@ -43,7 +43,8 @@ def rt_form():
     _lib.debug_set(_lib.EKS_DBG_RT_FORM, 0)
 
 
-@pytest.mark.parametrize("r,n,E", [(2, 2, 5), (2, 2, 7), (3, 8, 5), (3, 6, 4)])
+@pytest.mark.parametrize("r,n,E", [(2, 2, 5), (2, 2, 7), (3, 8, 5), (3, 6, 4), (3, 12, 5),
+                                   (3, 16, 3)])
 def test_runtime_n_kernel_equals_compiled(torch, rt_form, r, n, E):
     from eks_amd import batch, synthetic
     from oracle import eks_oracle as O
