@@ -647,9 +647,12 @@ def main():
     algo_used = int(_lib.load().eks_smooth_algo(*w["shape"], a.algo))
     w["key"] += f"-a{algo_used}"
 
+    tw = time.perf_counter()
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
+    # (a rough step time, only to size the pre-timing warm replays below)
+    step_est = (time.perf_counter() - tw) / max(1, a.warmup)
     assert_clean(torch, w, "warm-up")
     # the step's kernel sequence captured once as a HIP graph (hipGraph via
     # torch.cuda.CUDAGraph: the C ABI launches on the capturing stream and
@@ -669,13 +672,16 @@ def main():
             print(f"[bench] HIP graph capture failed ({exc}); launching eagerly",
                   file=sys.stderr)
     eager_step = step
+    warm_replays = 0
     if graph is not None:
         step = graph.replay
-        # the replays warmed right before the timed region as well: the first
-        # steps after the capture's idle gap run ~10 % slow while the GPU
-        # ramps (tools/first_step.py, profiles/r05/ab8), which W = 5 eager
-        # steps before the capture do not cover
-        for _ in range(a.warmup):
+        # the replays warmed right before the timed region as well: after the
+        # capture's idle gap the GPU runs ~7-10 % slow for the next ~10 ms of
+        # work (tools/first_step.py, profiles/r05/ab8), which W = 5 steps of
+        # a small shard (0.5 ms each) do not cover: at least W replays and
+        # at least ~30 ms of them (untimed; reported as warmup_replays)
+        warm_replays = max(a.warmup, min(200, int(math.ceil(0.03 / max(step_est, 1e-5)))))
+        for _ in range(warm_replays):
             step()
     dist.barrier()
     torch.cuda.synchronize()
@@ -710,9 +716,11 @@ def main():
             fit_step()
             e2e_smooth()
 
+        tw = time.perf_counter()
         for _ in range(max(1, a.warmup)):
             e2e_eager()
         torch.cuda.synchronize()
+        e2e_est = (time.perf_counter() - tw) / max(1, a.warmup)
         # replayed as one HIP graph like the hot-path step (eager: ~15 launches
         # whose host cost the small configurations would otherwise time)
         e2e_run = e2e_eager
@@ -724,7 +732,8 @@ def main():
                 ge.replay()
                 torch.cuda.synchronize()
                 e2e_run = ge.replay
-                for _ in range(max(1, a.warmup)):
+                # (warm as the hot-path replays above: >= W and >= ~30 ms)
+                for _ in range(max(a.warmup, min(200, int(math.ceil(0.03 / max(e2e_est, 1e-5)))))):
                     e2e_run()
             except Exception as exc:  # pragma: no cover - depends on the runtime
                 print(f"[bench] end-to-end graph capture failed ({exc}); launching eagerly",
@@ -818,6 +827,7 @@ def main():
                          setup_s, graph is not None, backend)
         if nll_rel is not None:
             line["nll_rel_diff_vs_cpu"] = nll_rel
+        line["warmup_replays"] = warm_replays
         print(json.dumps(line))
     dist.barrier()
 

@@ -142,7 +142,10 @@ EKS_DEV void frame_ensemble_raw(const T (&raw)[N][E], bool median, double (&y)[N
 // frames of member loads in flight per lane in k_fit_worst (compiled E: a
 // register ring; 4 x 10 loads at E = 5, n = 2.  Round 4's form loaded one
 // column of E members and waited for it: 5 loads in flight per wave, 4.2 TB/s)
-constexpr int kWorstD = 4;
+#ifndef EKS_WORST_D  // A/B builds only (tools/build_cur.sh)
+#define EKS_WORST_D 4
+#endif
+constexpr int kWorstD = EKS_WORST_D;
 static_assert(16 % kWorstD == 0, "the ring slots repeat every register tile");
 
 template <int E, int N, typename T, typename YT>
