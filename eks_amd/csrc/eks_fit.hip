@@ -1678,8 +1678,17 @@ __global__ __launch_bounds__(256) void k_fitw_final(long long B, const double *_
                                                     FitShift ks, int n, double smooth_param,
                                                     double *__restrict__ params,
                                                     int32_t *__restrict__ status) {
-  __shared__ double sA[kNW * kNW], sV[kNW * kNW], sM[kNW * kNW], sD[kNW * kNW], sEv[kNW];
+  // sA / sV double-buffered by round parity: a round's reads of one buffer
+  // are ordered before the next write of it by the following round's
+  // barrier, so one barrier per round
+  __shared__ double sA2[2][kNW * kNW], sV2[2][kNW * kNW];
+  __shared__ double sM[kNW * kNW], sD[kNW * kNW], sEv[kNW];
+  double *sV = sV2[0];
   __shared__ double sRed[2][4];
+  // the round-robin schedule, partner of index x in round k, tabulated once
+  // (runtime n: each entry takes three integer divisions, which on every
+  // thread's path of every round cost more than the rotation itself)
+  __shared__ unsigned char sPart[kNW - 1][kNW];
   const CsRt CS(n);
   const long long b = blockIdx.x;
   const int L = threadIdx.x, i = L / kNW, j = L % kNW;
@@ -1703,6 +1712,8 @@ __global__ __launch_bounds__(256) void k_fitw_final(long long B, const double *_
   const int Nm = n - 1;
   auto slot_of = [&](int x, int k) { return x == 0 ? 0 : 1 + (x - 1 + Nm - (k % Nm)) % Nm; };
   auto idx_at = [&](int pos, int k) { return pos == 0 ? 0 : 1 + (pos - 1 + k) % Nm; };
+  if (i < Nm && j < n) sPart[i][j] = (unsigned char)idx_at(Nm - slot_of(j, i), i);
+  __syncthreads();
   double off_prev = __builtin_inf();
   for (int sweep = 0; sweep < 60; ++sweep) {
     double off = (own && i < j) ? a * a : 0.0, dia = (own && i == j) ? a * a : 0.0;
@@ -1722,12 +1733,13 @@ __global__ __launch_bounds__(256) void k_fitw_final(long long B, const double *_
     if (off == 0.0 || off <= kJacobiTol * dia || off >= off_prev) break;  // block-uniform
     off_prev = off;
     for (int k = 0; k < Nm; ++k) {
+      const int pb = k & 1;
+      double *sA = sA2[pb], *sVb = sV2[pb];
       sA[L] = a;
-      sV[L] = v;
+      sVb[L] = v;
       __syncthreads();
-      auto partner = [&](int x) { return idx_at(Nm - slot_of(x, k), k); };
       const int li = own ? i : 0, lj = own ? j : 0;
-      const int pi = partner(li), pj = partner(lj);
+      const int pi = sPart[k][li], pj = sPart[k][lj];
       auto rot = [&](int x, int px, double &jxx, double &jpx) {
         const int p = x < px ? x : px, q = x < px ? px : x;
         const double apq = sA[p * kNW + q], app = sA[p * kNW + p], aqq = sA[q * kNW + q];
@@ -1740,8 +1752,7 @@ __global__ __launch_bounds__(256) void k_fitw_final(long long B, const double *_
       rot(li, pi, ji, jpi_i);
       rot(lj, pj, jj, jpj_j);
       const double a_ipj = sA[li * kNW + pj], a_pij = sA[pi * kNW + lj];
-      const double a_pipj = sA[pi * kNW + pj], v_ipj = sV[li * kNW + pj];
-      __syncthreads();
+      const double a_pipj = sA[pi * kNW + pj], v_ipj = sVb[li * kNW + pj];
       if (own) {
         const double r0 = a * jj + a_ipj * jpj_j;
         const double r1 = a_pij * jj + a_pipj * jpj_j;
@@ -1750,6 +1761,7 @@ __global__ __launch_bounds__(256) void k_fitw_final(long long B, const double *_
       }
     }
   }
+  __syncthreads();  // (the sweep cap: the last round's reads of sV2[0])
   sV[L] = v;
   sM[L] = Mij;
   sD[L] = Dij;
@@ -1806,6 +1818,8 @@ void fit_chunks(long long B, long long T, int &nc, long long &lc, int n = 0) {
   nc = (int)((T + lc - 1) / lc);
 }
 
+// (at six cameras' 782 partials, 28 per thread in two launches measured
+// slower than 16 in three: 0.031 -> 0.036 ms, profiles/r05/ab14)
 constexpr int kMergeFan = 16;
 
 // few long trajectories (B < 64: a trajectory-fastest wave would span
