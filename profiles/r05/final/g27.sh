@@ -1,11 +1,11 @@
-# Round 5 final evidence of the shipped build (round-5 tail: compiled n = 12,
+# Round 5 final evidence of the shipped build (after the rejected split-selection fusion):
 # -m gpu suite, smoke, the default bench line (CPU baseline), configs 2 / 3
 # (4, 6, 8 cameras) / 5, the 4- / 8-GPU shard sizes, T = 4 000, rocprofv3
 # kernel traces + FETCH / WRITE passes of config 4 and its 8-GPU shard, and
 # the SQ / VALU passes of algo 3.
 set -o pipefail
 export PYTHONDONTWRITEBYTECODE=1 TMPDIR=/tmp
-O=gpurun_out/g20; mkdir -p $O
+O=gpurun_out/g27; mkdir -p $O
 summ() { python - "$1" "$2" <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
@@ -36,4 +36,6 @@ unset EKS_LIB
 bash tools/gpu_profile.sh r05c4 > $O/profile_c4.log 2>&1 || exit $?
 BENCH_ARGS="--videos 128" bash tools/gpu_profile.sh r05v128 > $O/profile_v128.log 2>&1 || exit $?
 TAG=r05 bash tools/gpu_pmc.sh > $O/pmc.log 2>&1 || exit $?
+BENCH_ARGS="--config 5" bash tools/gpu_profile.sh r05c5 > $O/profile_c5.log 2>&1 || exit $?
+BENCH_ARGS="--config 3 --cameras 6" bash tools/gpu_profile.sh r05c3v6 > $O/profile_c3v6.log 2>&1 || exit $?
 echo done

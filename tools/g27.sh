@@ -36,4 +36,6 @@ unset EKS_LIB
 bash tools/gpu_profile.sh r05c4 > $O/profile_c4.log 2>&1 || exit $?
 BENCH_ARGS="--videos 128" bash tools/gpu_profile.sh r05v128 > $O/profile_v128.log 2>&1 || exit $?
 TAG=r05 bash tools/gpu_pmc.sh > $O/pmc.log 2>&1 || exit $?
+BENCH_ARGS="--config 5" bash tools/gpu_profile.sh r05c5 > $O/profile_c5.log 2>&1 || exit $?
+BENCH_ARGS="--config 3 --cameras 6" bash tools/gpu_profile.sh r05c3v6 > $O/profile_c3v6.log 2>&1 || exit $?
 echo done
