@@ -423,7 +423,7 @@ __global__ __launch_bounds__(BLK) void k_fit_select(const double *__restrict__ w
   // row's frame mask (T <= kLdsMaskT: at most 1024 words).  Rows shorter
   // than 65 536 frames (the 256-thread kernel) count in 16-bit halves of the
   // words: 8 KB instead of 16, four blocks per CU instead of three.
-  constexpr bool kPacked = BLK == 256;
+  constexpr bool kPacked = BLK == 256 || BLK == 512;
   __shared__ unsigned hist[kPacked ? kBins / 2 : kBins];
   auto hcount = [&](unsigned d) -> unsigned {
     return kPacked ? (hist[d >> 1] >> ((d & 1u) << 4)) & 0xffffu : hist[d];
@@ -638,6 +638,12 @@ __global__ __launch_bounds__(BLK) void k_fit_select(const double *__restrict__ w
 // Same threshold and mask bits as k_fit_select (tests/test_gpu_fit_mask.py).
 // ---------------------------------------------------------------------------
 constexpr long long kSelSplitB = 512;
+// threads of the one-block-per-row selection for rows of 4 097 .. 65 535
+// frames (A/B builds: -DEKS_SEL_BLK=512)
+#ifndef EKS_SEL_BLK
+#define EKS_SEL_BLK 256
+#endif
+constexpr int kSelBlk = EKS_SEL_BLK;
 }  // namespace
 // eks_debug_set(EKS_DBG_FIT_SELECT): 0 automatic, 1 one block per row, 2 split
 long long g_fit_select = 0;
@@ -1967,8 +1973,8 @@ extern "C" int eks_fit(const void *obs, int obs_dtype, int64_t B, int64_t T, int
       hipLaunchKernelGGL((k_fit_select<256, 16>), dim3((unsigned)B), dim3(256), 0, s, worst, T, lo,
                          hi, g, thr, yev ? kept : nullptr, W);
     } else {
-      hipLaunchKernelGGL(k_fit_select<256>, dim3((unsigned)B), dim3(256), 0, s, worst, T, lo,
-                         hi, g, thr, yev ? kept : nullptr, W);
+      hipLaunchKernelGGL(k_fit_select<kSelBlk>, dim3((unsigned)B), dim3(kSelBlk), 0, s, worst, T,
+                         lo, hi, g, thr, yev ? kept : nullptr, W);
     }
     return check_launch("k_fit_select");
   };
