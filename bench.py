@@ -612,8 +612,12 @@ def make_line(a, w, world, algo_used, units_local, units_total, elapsed_max, ker
         line["distributed"] = dict(world_size=world, backend=backend, units_per_rank=units_local,
                                    roofline_scope="rank 0's launch (per-rank shard)")
     if gather_ms is not None:
+        # config 4 is "sharded over N GPUs (RCCL gather)": the rate with the
+        # one gather of every output to rank 0 priced in (once per job, not
+        # per step: kp-ts over the step time plus the gather time)
         line["gather_ms"] = gather_ms
         line["gather_bytes"] = gather_bytes
+        line["value_with_gather"] = units_total / (elapsed_max / a.steps + gather_ms * 1e-3)
     return line
 
 

@@ -298,13 +298,35 @@ EKS_DEV void jacobi_cs(double app, double aqq, double apq, double &c, double &s)
   c = 1.0;
   s = 0.0;
   if (apq == 0.0) return;
-  const double d = aqq - app, h = 2.0 * apq;
-  const double x = fma(d, d, h * h);
+  double d = aqq - app, h = 2.0 * apq;
+  double x = fma(d, d, h * h);
+  if (!(x >= 0x1p-1000 && x <= 0x1p1000)) {
+    // |d|, |h| below ~1e-151 or above ~1e150: x under- / overflows and r
+    // would be 0 * inf.  t is invariant under a common scaling of d and h,
+    // so rescale both by the power of two of the larger (exact; the
+    // matrices are pre-scaled by pca_scale, so this is a backstop)
+    int e;
+    (void)frexp(fmax(fabs(d), fabs(h)), &e);
+    d = ldexp(d, -e);
+    h = ldexp(h, -e);
+    x = fma(d, d, h * h);
+  }
   const double r = x * nr_rsq(x);  // sqrt(d^2 + h^2)
   double t = fabs(h) * nr_rcp(fabs(d) + r);
   if (d != 0.0 && ((d < 0.0) != (h < 0.0))) t = -t;  // theta < 0
   c = nr_rsq(fma(t, t, 1.0));
   s = t * c;
+}
+
+// The power of two 2^-e that brings the largest |entry| of the PCA's scatter
+// matrix into [0.5, 1): the Jacobi then runs on exactly scaled entries (the
+// rotations and the eigenvalue order are invariant under it; without it the
+// squared off-diagonal mass of a matrix with entries below ~1e-154
+// underflows to 0 and the sweeps stop before rotating).  m: the max |entry|
+EKS_DEV int pca_scale(double m) {
+  int e = 0;
+  if (m > 0.0 && m <= __DBL_MAX__) (void)frexp(m, &e);
+  return e;
 }
 
 // lane 0 of the wave's active lanes (the writer of a ballot word)
@@ -1330,6 +1352,12 @@ __global__ __launch_bounds__(64) void k_fit_final(long long B, const double *__r
     // principal axes of the good-frame scatter matrix (sklearn's PCA axes
     // up to sign; outputs do not depend on the sign)
     double a = Mij, v = (own && i == j) ? 1.0 : 0.0;
+    {
+      double m = own ? fabs(a) : 0.0;
+#pragma unroll
+      for (int w = 32; w >= 1; w >>= 1) m = fmax(m, __shfl_xor(m, w, 64));
+      a = ldexp(a, -pca_scale(m));
+    }
     // parallel cyclic Jacobi (round-robin ordering): each sweep is N - 1
     // rounds of N / 2 disjoint rotations, applied at once as A <- J^T A J,
     // V <- V J (lane (i, j) combines the entries of its row pair x column
@@ -1715,6 +1743,16 @@ __global__ __launch_bounds__(256) void k_fitw_final(long long B, const double *_
   if (L < R * R) pr[pA + L] = (L / R == L % R) ? 1.0 : 0.0;
   if (L < n) pr[pOff + L] = ks.K[b * n + L] + o[CS.mean + L] / cnt;
   double a = Mij, v = (own && i == j) ? 1.0 : 0.0;
+  {  // the exact power-of-two pre-scaling of k_fit_final (pca_scale)
+    double m = own ? fabs(a) : 0.0;
+#pragma unroll
+    for (int w = 32; w >= 1; w >>= 1) m = fmax(m, __shfl_xor(m, w, 64));
+    if ((L & 63) == 0) sRed[0][L >> 6] = m;
+    __syncthreads();
+    m = fmax(fmax(sRed[0][0], sRed[0][1]), fmax(sRed[0][2], sRed[0][3]));
+    __syncthreads();
+    a = ldexp(a, -pca_scale(m));
+  }
   const int Nm = n - 1;
   auto slot_of = [&](int x, int k) { return x == 0 ? 0 : 1 + (x - 1 + Nm - (k % Nm)) % Nm; };
   auto idx_at = [&](int pos, int k) { return pos == 0 ? 0 : 1 + (pos - 1 + k) % Nm; };

@@ -95,8 +95,8 @@ static int smooth_call(const void *obs, int obs_dtype, int64_t B, int64_t T, int
   const bool rt = use_rt(r, n, algo);
   if (!rt && !shape_compiled(r, n))
     return set_err(EKS_ERR_UNSUPPORTED,
-                   "eks_smooth: (r=%d, n=%d) not supported (compiled: (2,2) (3,4) (3,6) (3,8); "
-                   "any n <= %d for r = 2, 3)", r, n, kMaxObsRt);
+                   "eks_smooth: (r=%d, n=%d) not supported (compiled: (2,2) (3,4) (3,6) (3,8) "
+                   "(3,12) (3,16); any n <= %d for r = 2, 3)", r, n, kMaxObsRt);
   if (rt && phase)
     return set_err(EKS_ERR_UNSUPPORTED, "eks_smooth_seg: (r=%d, n=%d) has no time-parallel kernels", r, n);
   if ((model_flags & EKS_MODEL_C_IDENTITY) && r != n)

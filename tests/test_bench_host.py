@@ -6,6 +6,7 @@ import os
 import sys
 
 import numpy as np
+import pytest
 
 import bench
 from eks_amd import synthetic
@@ -107,6 +108,8 @@ def test_multi_rank_line_schema(tmp_path, monkeypatch):
     assert line["roofline"]["traffic"] == 2.5e9
     assert line["distributed"]["world_size"] == 8 and line["distributed"]["backend"] == "nccl"
     assert line["gather_ms"] == 3.2 and line["gather_bytes"] == 2.79e9
+    # the gather priced into the rate: kp-ts over (step time + gather time)
+    assert line["value_with_gather"] == pytest.approx(17408 * 10000 / (0.01 + 3.2e-3))
     assert line["value"] == 17408 * 10000 / 0.01
     # the N = 1 line of the full batch looks up its own entry
     assert bench.load_pmc("config4-singleview-v1024-k17-e5-t10000-a3", str(pmc)) is None

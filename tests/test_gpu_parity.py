@@ -703,6 +703,34 @@ def test_fit_multicam_vs_host(torch, V, T):
         _close(got["Q"] * np.outer(sgn, sgn), ref["Q"], rtol=1e-7)
 
 
+@pytest.mark.parametrize("V", [2, 6])
+def test_fit_multicam_tiny_scale_pca(torch, V):
+    """Members scaled by 2^-280 (scatter entries ~1e-165: d^2 + h^2 of a
+    Jacobi rotation underflows, round-5 advisor finding): the PCA runs on
+    exactly pre-scaled matrices (eks_fit.hip pca_scale), so the fit equals the
+    unscaled one scaled by the same power of two -- axes, offsets, Q, S0.
+    V = 2 runs k_fit_final, V = 6 the wide k_fitw_final."""
+    from eks_amd import batch, synthetic
+    rng = np.random.default_rng(40 + V)
+    st = synthetic.multiview_obs(rng, V, 5, 600, K=2).astype(np.float64)  # (E, T, K, 2V)
+    stacks = np.ascontiguousarray(st.transpose(2, 0, 1, 3))
+    n = 2 * V
+    sc = 2.0 ** -280
+    fits = []
+    for x in (stacks, stacks * sc):
+        obs = torch.from_numpy(x).cuda().permute(0, 2, 1, 3)
+        fits.append(batch.fit(obs, kind="multicam", n=n, r=3, smooth_param=0.01,
+                              quantile_keep=25)[0].cpu().numpy())
+    for k in range(2):
+        a, b = _unpack(fits[0][k], n, 3), _unpack(fits[1][k], n, 3)
+        assert np.isfinite(fits[1][k]).all()
+        sgn = np.sign(np.sum(a["C"] * b["C"], axis=0))
+        _close(b["C"] * sgn, a["C"], rtol=1e-12)
+        _close(b["offset"] / sc, a["offset"], rtol=1e-12)
+        _close(b["S0"] / sc ** 2, a["S0"], rtol=1e-12)
+        _close(b["Q"] * np.outer(sgn, sgn) / sc ** 2, a["Q"], rtol=1e-12)
+
+
 def test_fit_then_smooth_matches_singleview_golden(torch):
     """eks_fit + eks_smooth reproduce the committed single-view goldens."""
     from eks_amd import batch

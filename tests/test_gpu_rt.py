@@ -170,3 +170,68 @@ def test_wide_fit_handoff_then_time_parallel_smooth(torch, V, E, dtype):
     c = batch.smooth(yev, params, n=n, r=3, want_nll=True, check=True)
     assert float((c["out"] - a["out"]).abs().max()) < 1e-8
     torch.testing.assert_close(c["nll"], a["nll"], rtol=1e-10, atol=0)
+
+
+def _multicam_batch(rng, V, E, B, T):
+    from eks_amd import batch, synthetic
+    from oracle import eks_oracle as O
+    st = synthetic.multiview_obs(rng, V, E, T, K=B).transpose(2, 0, 1, 3)
+    models = []
+    for b in range(B):
+        preds, ev = O.ensemble_array(st[b].astype(np.float64))
+        models.append(O.multicam_params(preds, ev, 0.01, 25))
+    stk = lambda k: np.stack([m[k] for m in models])  # noqa: E731
+    params = batch.pack_params(stk("m0"), stk("S0"), stk("A"), stk("Q"), stk("C"), stk("means"))
+    return st, params, batch.model_flags(stk("A"), stk("C"))
+
+
+@pytest.mark.parametrize("n,B,T", [(12, 6, 3000), (12, 256, 400), (16, 4, 2500), (16, 264, 300)])
+def test_compiled_wide_shapes_time_parallel_vs_sequential(torch, n, B, T):
+    """Six- and eight-camera calls run compiled (r, n) = (3, 12) / (3, 16)
+    kernels (eks_shape_312.hip / eks_shape_316.hip).  Explicit algo 2 and
+    algo 3 from the member predictions -- few trajectories (group mode) and
+    B >= 256 (whole-block chunks, k3_bwd's __launch_bounds__(256, 2)) --
+    against algo 1: outputs, latent means and NLL at the compiled
+    time-parallel tolerances (tests/test_gpu_configs.py PX_ALGO, NLL_RTOL)."""
+    from eks_amd import batch
+    rng = np.random.default_rng(n * 7 + B)
+    st, params, flags = _multicam_batch(rng, n // 2, 5, B, T)
+    d = batch.make_time_major(st, dtype=np.float32)
+    ref = batch.smooth(d, params, n=n, r=3, algo=1, flags=flags, want_nll=True, want_ms=True,
+                       check=True)
+    for algo in (2, 3):
+        res = batch.smooth(d, params, n=n, r=3, algo=algo, flags=flags, want_nll=True,
+                           want_ms=True)
+        assert int((res["status"] != 0).sum()) == 0, algo
+        assert float((res["out"] - ref["out"]).abs().max()) < 1e-8, algo
+        assert float((res["ms"] - ref["ms"]).abs().max()) < 1e-8, algo
+        rel = float(((res["nll"] - ref["nll"]) / ref["nll"]).abs().max())
+        assert rel < 1e-10, (algo, rel)
+
+
+@pytest.mark.parametrize("n", [12, 16])
+def test_compiled_wide_shapes_segmented(torch, n):
+    """The phased time-shard path (eks_smooth_seg phases 1-3 + eks_seg_combine)
+    at the compiled n = 12 / 16 shapes against the one-piece sequential call."""
+    from eks_amd import batch, timeshard
+    rng = np.random.default_rng(100 + n)
+    st, params, flags = _multicam_batch(rng, n // 2, 5, 2, 6000)
+    d = batch.make_time_major(st, dtype=np.float32)
+    ref = batch.smooth(d, params, n=n, r=3, algo=1, flags=flags, want_nll=True, want_ms=True,
+                       check=True)
+    seg = timeshard.smooth_segments(d, params, n=n, r=3, nseg=3, flags=flags, want_ms=True)
+    assert int((seg["status"] != 0).sum()) == 0
+    assert float((seg["out"] - ref["out"]).abs().max()) < 1e-8
+    assert float((seg["ms"] - ref["ms"]).abs().max()) < 1e-8
+    np.testing.assert_allclose(seg["nll"].cpu().numpy(), ref["nll"].cpu().numpy(), rtol=1e-10)
+
+
+def test_unsupported_shape_message_lists_compiled_shapes(torch):
+    from eks_amd import _lib, batch
+    rng = np.random.default_rng(3)
+    st, params, flags = _multicam_batch(rng, 2, 3, 1, 50)
+    d = batch.make_time_major(st, dtype=np.float32)
+    # r = 4 has no kernels at all: the error lists the compiled shapes
+    bad = torch.zeros((1, batch.param_len(4, 4)), dtype=torch.float64, device="cuda")
+    with pytest.raises(_lib.EksError, match=r"\(3,12\) \(3,16\)"):
+        batch.smooth(d, bad, n=4, r=4, algo=2, flags=0)

@@ -27,7 +27,7 @@ pass() {  # name, counters...
 }
 pass sq SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY \
      SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_VALU GRBM_GUI_ACTIVE GRBM_COUNT || exit $?
-pass lvl SQ_LEVEL_WAVES SQ_ACCUM_PREV_HIRES SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS \
+pass lvl SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS \
      SQ_INSTS_SALU GRBM_GUI_ACTIVE || true
 pass valu VALUBusy || true
 pass mem MemUnitStalled || true

@@ -6,6 +6,8 @@ import os
 import sys
 from collections import defaultdict
 
+N_XCD, N_SIMD = 8, 256 * 4  # MI355X
+
 
 def main(d):
     acc = defaultdict(lambda: defaultdict(list))  # kernel -> counter -> per-dispatch values
@@ -28,10 +30,19 @@ def main(d):
             print(f"  VALU active / wave cycles    {cnt['SQ_ACTIVE_INST_VALU'] / cnt['SQ_WAVE_CYCLES']:.3f}")
         if "SQ_WAIT_ANY" in cnt and cnt.get("SQ_WAVE_CYCLES"):
             print(f"  wait-any / wave cycles       {cnt['SQ_WAIT_ANY'] / cnt['SQ_WAVE_CYCLES']:.3f}")
-        if "SQ_ACCUM_PREV_HIRES" in cnt and cnt.get("GRBM_GUI_ACTIVE"):
-            # SQ_LEVEL_WAVES accumulated per cycle (summed over SEs / XCDs) / 256 CUs / 4 SIMDs
-            print(f"  mean waves per SIMD (approx) {cnt['SQ_ACCUM_PREV_HIRES'] / cnt['GRBM_GUI_ACTIVE'] / 1024:.3f}")
-
+        if "SQ_WAVE_CYCLES" in cnt and cnt.get("GRBM_GUI_ACTIVE"):
+            # SQ_WAVE_CYCLES counts quad-cycles, summed over every resident
+            # wave; GRBM_GUI_ACTIVE is the sum over the 8 XCDs
+            # (MI355X_MICROARCH.md, s_memtime vs SQ PMC units; DVFS
+            # give-back): mean resident waves per SIMD over the dispatch =
+            # 4 * SQ_WAVE_CYCLES / (GRBM_GUI_ACTIVE / 8) / (256 CUs * 4 SIMDs).
+            # (SQ_LEVEL_WAVES / SQ_ACCUM_PREV_HIRES read 0 on gfx950.)
+            occ = 4.0 * cnt["SQ_WAVE_CYCLES"] / (cnt["GRBM_GUI_ACTIVE"] / N_XCD) / N_SIMD
+            print(f"  mean waves per SIMD          {occ:.3f}")
+            if cnt.get("SQ_WAVES"):
+                # a persistent grid keeps every wave resident for the whole
+                # dispatch: SQ_WAVES / SIMDs is the launch-bounds figure
+                print(f"  SQ_WAVES / SIMDs             {cnt['SQ_WAVES'] / N_SIMD:.3f}")
 
 if __name__ == "__main__":
     main(sys.argv[1])
