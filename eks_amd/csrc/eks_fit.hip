@@ -142,11 +142,21 @@ EKS_DEV void frame_ensemble_raw(const T (&raw)[N][E], bool median, double (&y)[N
 // frames of member loads in flight per lane in k_fit_worst (compiled E: a
 // register ring; 4 x 10 loads at E = 5, n = 2.  Round 4's form loaded one
 // column of E members and waited for it: 5 loads in flight per wave, 4.2 TB/s)
-#ifndef EKS_WORST_D  // A/B builds only (tools/build_cur.sh)
+// The depth follows the frame's size (round 6, advisor finding): ~160 bytes
+// of member values per lane in flight (4 frames at n = 2 float32, 2 at
+// n = 4, 1 at n >= 6 or E x n x 8 > 80 bytes) -- a fixed depth of 4 held
+// 4 E n values in registers and spilled every n >= 4 instantiation into
+// AGPRs at one wave per SIMD (n = 8, E = 5: 256 VGPRs + 101 AGPRs).
+#ifndef EKS_WORST_D  // A/B builds only (tools/build_cur.sh): the n = 2 depth
 #define EKS_WORST_D 4
 #endif
-constexpr int kWorstD = EKS_WORST_D;
-static_assert(16 % kWorstD == 0, "the ring slots repeat every register tile");
+template <int E, int N, typename T>
+constexpr int worst_depth() {
+  constexpr int bytes = (E > 0 ? E : 1) * N * (int)sizeof(T);
+  constexpr int d = 160 / bytes;
+  return d >= EKS_WORST_D ? EKS_WORST_D : d >= 2 ? 2 : 1;
+}
+static_assert(16 % EKS_WORST_D == 0, "the ring slots repeat every register tile");
 
 template <int E, int N, typename T, typename YT>
 __global__ __launch_bounds__(256) void k_fit_worst(const T *__restrict__ obs, FitShape sh,
@@ -186,6 +196,7 @@ __global__ __launch_bounds__(256) void k_fit_worst(const T *__restrict__ obs, Fi
   // compiled E: the lane's frames stream through a ring kWorstD frames deep
   // (reads past the lane's last frame are clamped to it: cache hits)
   constexpr int RE = E > 0 ? E : 1;
+  constexpr int kWorstD = worst_depth<E, N, T>();
   T ring[kWorstD][N][RE];
   auto fetch = [&](int slot, long long u) {
     u = u < t1 ? u : t1 - 1;

@@ -83,9 +83,18 @@ struct F32MinMax {
 // middle ones for even E)
 template <int E, typename T>
 EKS_DEV double median_of(const T (&raw)[E]) {
-  if constexpr (std::is_same<T, float>::value && (E == 3 || E == 5)) {
+  if constexpr (std::is_same<T, float>::value && (E == 3 || E == 4 || E == 5)) {
     if constexpr (E == 3) {  // 1 v_med3_f32
       return (double)__builtin_amdgcn_fmed3f(raw[0], raw[1], raw[2]);
+    } else if constexpr (E == 4) {
+      // the two middle values of four are {max(p, q), min(P, Q)} for the
+      // pairs' minima p, q and maxima P, Q (4 med3 + 2 instead of a sorting
+      // network); numpy's mean of the two, (s1 + s2) / 2 (the addition
+      // commutes, so their order does not matter)
+      const F32MinMax f;
+      const float a = f.mx(f.mn(raw[0], raw[1]), f.mn(raw[2], raw[3]));
+      const float b = f.mn(f.mx(raw[0], raw[1]), f.mx(raw[2], raw[3]));
+      return ((double)a + (double)b) / 2.0;
     } else {  // 7: drop the min and max of s0..s3, then the median of 3
       const F32MinMax f;
       const float lo = f.mx(f.mn(raw[0], raw[1]), f.mn(raw[2], raw[3]));
