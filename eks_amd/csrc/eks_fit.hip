@@ -262,10 +262,9 @@ __global__ __launch_bounds__(256) void k_fit_worst(const T *__restrict__ obs, Fi
 // between the unrolled body and the tail loop (a split wave would ballot in
 // two halves, and the two writers of the mask word would overwrite each
 // other's frames).
-template <int BLK, typename K, typename F>
+template <int BLK, int U = kSelU, typename K, typename F>
 EKS_DEV void for_keys(const K *keys, long long n, F &&f) {
   static_assert(BLK % 64 == 0, "whole waves");
-  constexpr int U = kSelU;
   long long i = threadIdx.x;
   for (; (i | 63) + (U - 1) * BLK < n; i += U * BLK) {
     K x[U];
@@ -426,8 +425,8 @@ EKS_DEV K block_select(const K *keys, long long n, long long k, int top,
   return prefix;
 }
 
-// One block per trajectory.  Pass 1 histograms the top digit (bits 51-62:
-// exponent and first mantissa bit; variances are >= 0 so bit patterns sort
+// One block per trajectory.  Pass 1 histograms the top digit (bits 50-62:
+// exponent and first two mantissa bits; variances are >= 0 so bit patterns sort
 // like values) over the row in global memory; pass 2 compacts the keys of
 // the bin holding rank `lo` into LDS (with their frame indices) and sets the
 // kept-frame bits of every frame below that bin; the remaining digits and the
@@ -438,42 +437,91 @@ EKS_DEV K block_select(const K *keys, long long n, long long k, int top,
 // buffer falls back to selecting over the global row, and a row too long for
 // 16-bit indices (or a threshold equal to a key above the bin) marks the
 // frames in one more pass over the row.
-constexpr int kCand = 3072;        // LDS candidates (24 KB + 6 KB of indices)
+//
+// LDS (round 6): the top digit is 13 bits (bits 50-62) and the bin's
+// candidates are compacted into the histogram's own LDS once the bin is
+// known, so a 256-thread block needs ~20 KB instead of ~39 KB and a CU holds
+// twice the rows in flight (the passes are latency bound per row: round 5's
+// 512-thread and register-resident forms, with fewer rows per CU, were
+// slower in proportion).  EKS_SEL_COMPACT=0 builds round 5's layout (12-bit
+// digit, 3 072 candidates beside the histogram) for A/B runs.
+#ifndef EKS_SEL_COMPACT
+#define EKS_SEL_COMPACT 1
+#endif
+constexpr bool kSelCompact = EKS_SEL_COMPACT != 0;
+constexpr int kSelTopBits = kSelCompact ? 13 : 12;  // top digit: bits 63-kSelTopBits .. 62
+constexpr int kSelBins = 1 << kSelTopBits;
+constexpr int kCand = kSelCompact ? 1536 : 3072;    // LDS candidates (+ 16-bit indices)
 constexpr int kSelDigit = 8;       // digits of the in-LDS select (1 KB histogram)
-constexpr long long kLdsMaskT = 65536;  // rows with 16-bit frame indices
+// rows with 16-bit frame indices and an LDS frame mask (2 KB / 8 KB)
+constexpr long long kLdsMaskT = kSelCompact ? 16384 : 65536;
 
 // KPT > 0 (rows of at most BLK * KPT frames): the row is read ONCE, into
 // KPT registers per thread, and both passes (histogram, compaction + mask)
 // run over the registers -- round 4's form read the row from memory twice
 // (1.93x the worst plane's bytes at config 4).  KPT = 0: the passes read
 // the row from memory (longer rows).
+// waves per SIMD the selection is compiled for (its VGPR budget: 64 at 8):
+// the compact layout's ~20 KB of LDS allows 8 blocks of 256 threads per CU.
+// Config 4 (17 408 rows of 10 000 frames), alternated on one box:
+// k_fit_select 0.765-0.771 ms (round 5's layout, 4 blocks per CU) -> 0.565
+// (compact, 6) -> 0.504-0.511 (compact, 8); profiles/r06/ab_fit/README.md
+#ifndef EKS_SEL_WPE
+#define EKS_SEL_WPE (EKS_SEL_COMPACT ? 8 : 1)
+#endif
+// key loads in flight per thread of the selection's row passes (compact
+// layout: twice the blocks per CU, so half of kSelU keeps the bytes in flight)
+#ifndef EKS_SEL_U
+#define EKS_SEL_U 8
+#endif
+constexpr int kSelRowU = kSelCompact ? EKS_SEL_U : kSelU;
 template <int BLK, int KPT = 0>
-__global__ __launch_bounds__(BLK) void k_fit_select(const double *__restrict__ worst,
+__global__ __launch_bounds__(BLK, EKS_SEL_WPE) void k_fit_select(const double *__restrict__ worst,
                                                     long long TT, long long lo, long long hi,
                                                     double g, double *__restrict__ thr,
                                                     uint64_t *__restrict__ kept, long long W) {
   // the top-digit histogram; after the bin is found the same LDS holds the
-  // row's frame mask (T <= kLdsMaskT: at most 1024 words).  Rows shorter
-  // than 65 536 frames (the 256-thread kernel) count in 16-bit halves of the
-  // words: 8 KB instead of 16, four blocks per CU instead of three.
+  // bin's candidates (compact layout) or the row's frame mask (round 5's).
+  // Rows shorter than 65 536 frames (the 256-thread kernel) count in 16-bit
+  // halves of the words.
   constexpr bool kPacked = BLK == 256 || BLK == 512;
-  __shared__ unsigned hist[kPacked ? kBins / 2 : kBins];
+  constexpr int kHistWords = kPacked ? kSelBins / 2 : kSelBins;
+  constexpr int kCandBytes = kCand * (int)(sizeof(uint64_t) + sizeof(uint16_t));
+  // compact layout: the candidates (keys, then 16-bit frame indices) reuse
+  // the histogram's words once the bin is found; the frame mask has its own
+  constexpr int kHistAlloc =
+      kSelCompact && kCandBytes > kHistWords * 4 ? (kCandBytes + 3) / 4 : kHistWords;
+  __shared__ __attribute__((aligned(16))) unsigned hist[kHistAlloc];
   auto hcount = [&](unsigned d) -> unsigned {
     return kPacked ? (hist[d >> 1] >> ((d & 1u) << 4)) & 0xffffu : hist[d];
   };
   __shared__ unsigned hsel[1 << kSelDigit];
-  __shared__ uint64_t cand[kCand];
-  __shared__ uint16_t cidx[kCand];
   __shared__ uint64_t su[4];
   __shared__ long long si[2 + BLK / 64];
   __shared__ double sthr;
   __shared__ unsigned ncand;
   __shared__ int any_nan;
-  static_assert(kLdsMaskT / 64 * sizeof(uint64_t) <= sizeof(hist), "mask fits the histogram");
+  uint64_t *cand;
+  uint16_t *cidx;
+  uint64_t *smask;
+  if constexpr (kSelCompact) {
+    static_assert(kCandBytes <= (int)sizeof(hist), "candidates fit the histogram's LDS");
+    __shared__ uint64_t smask_own[kLdsMaskT / 64];
+    cand = reinterpret_cast<uint64_t *>(hist);
+    cidx = reinterpret_cast<uint16_t *>(cand + kCand);
+    smask = smask_own;
+  } else {
+    __shared__ uint64_t cand_own[kCand];
+    __shared__ uint16_t cidx_own[kCand];
+    static_assert(kLdsMaskT / 64 * sizeof(uint64_t) <= sizeof(hist), "mask fits the histogram");
+    cand = cand_own;
+    cidx = cidx_own;
+    smask = reinterpret_cast<uint64_t *>(hist);
+  }
   const long long b = blockIdx.x;
   const uint64_t *keys = reinterpret_cast<const uint64_t *>(worst + b * TT);
   uint64_t *krow = kept ? kept + b * W : nullptr;
-  constexpr int lo_bit = 51;
+  constexpr int lo_bit = 63 - kSelTopBits;
   // the row's keys in registers (KPT > 0): key threadIdx.x + u * BLK in
   // xr[u]; every load issued at once.  Past the row: +inf bit patterns
   // above every variance (never counted: the loops below test the index).
@@ -497,10 +545,10 @@ __global__ __launch_bounds__(BLK) void k_fit_select(const double *__restrict__ w
         if ((long long)(threadIdx.x & ~63u) + (long long)u * BLK < TT) f(xr[u], i, i < TT);
       }
     } else {
-      for_keys<BLK>(keys, TT, [&](uint64_t x, long long i) { f(x, i, true); });
+      for_keys<BLK, kSelRowU>(keys, TT, [&](uint64_t x, long long i) { f(x, i, true); });
     }
   };
-  for (unsigned i = threadIdx.x; i < (kPacked ? kBins / 2 : kBins); i += BLK) hist[i] = 0;
+  for (unsigned i = threadIdx.x; i < (unsigned)kHistWords; i += BLK) hist[i] = 0;
   if (threadIdx.x == 0) {
     any_nan = 0;
     ncand = 0;
@@ -511,7 +559,7 @@ __global__ __launch_bounds__(BLK) void k_fit_select(const double *__restrict__ w
   row_keys([&](uint64_t x, long long, bool valid) {
     if (!valid) return;
     nan |= (x & 0x7fffffffffffffffull) > 0x7ff0000000000000ull;
-    const unsigned d = (unsigned)(x >> lo_bit) & (kBins - 1);
+    const unsigned d = (unsigned)(x >> lo_bit) & (kSelBins - 1);
     if constexpr (kPacked)
       atomicAdd(&hist[d >> 1], 1u << ((d & 1u) << 4));  // counts <= T < 65 536
     else
@@ -527,7 +575,7 @@ __global__ __launch_bounds__(BLK) void k_fit_select(const double *__restrict__ w
   }
   // bin of rank lo (parallel scan over the histogram)
   {
-    constexpr unsigned per = kBins / BLK;
+    constexpr unsigned per = kSelBins / BLK;
     long long mine = 0;
     for (unsigned d = threadIdx.x * per; d < (threadIdx.x + 1) * per; ++d) mine += hcount(d);
     long long total;
@@ -547,7 +595,6 @@ __global__ __launch_bounds__(BLK) void k_fit_select(const double *__restrict__ w
   __syncthreads();
   const bool in_lds = cnt_bin <= kCand;
   const bool lds_mask = krow && in_lds && TT <= kLdsMaskT;
-  uint64_t *smask = reinterpret_cast<uint64_t *>(hist);
   uint64_t ka;
   long long le_in_bin = -1;  // keys of the bin <= ka (when resolved in LDS)
   uint64_t above_in_bin = ~0ull;
@@ -613,7 +660,7 @@ __global__ __launch_bounds__(BLK) void k_fit_select(const double *__restrict__ w
       }
       __syncthreads();
       unsigned long long c = 0, ab = ~0ull;
-      for_keys<BLK>(keys, TT, [&](uint64_t x, long long) {
+      for_keys<BLK, kSelRowU>(keys, TT, [&](uint64_t x, long long) {
         c += x <= ka;
         if (x > ka && x < ab) ab = x;
       });
@@ -644,7 +691,7 @@ __global__ __launch_bounds__(BLK) void k_fit_select(const double *__restrict__ w
     __syncthreads();
     for (long long w = threadIdx.x; w < W; w += BLK) krow[w] = smask[w];
   } else {
-    for_keys<BLK>(keys, TT, [&](uint64_t x, long long i) {
+    for_keys<BLK, kSelRowU>(keys, TT, [&](uint64_t x, long long i) {
       const uint64_t m = __ballot(__longlong_as_double((long long)x) <= th);
       if (first_active_lane()) krow[i >> 6] = m;
     });
