@@ -77,9 +77,21 @@ static __device__ unsigned long long g_stamps[2 * kStampBlocks * kStampIts * 32]
                (threadIdx.x >> 6) * 8 + (K)] =                                               \
           (K) == 0 ? (((unsigned long long)wk.grp << 32) | (unsigned long long)wk.c) : t_;    \
   } while (0)
+// wave 0's chain detail (after both waves' slot-0 words are written at the
+// unit's start): the look-back's end time into wave 1's slot 0, the number
+// of units folded into wave 2's
+#define EKS_STAMP_AUX(PASS, WSLOT, VAL)                                                       \
+  do {                                                                                        \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < kStampBlocks && it < kStampIts)               \
+      g_stamps[(((size_t)(PASS) * kStampBlocks + blockIdx.x) * kStampIts + it) * 32 +        \
+               (WSLOT) * 8] = (unsigned long long)(VAL);                                     \
+  } while (0)
 #else
 #define EKS_STAMP(PASS, K) \
   do {                     \
+  } while (0)
+#define EKS_STAMP_AUX(PASS, WSLOT, VAL) \
+  do {                                  \
   } while (0)
 #endif
 
@@ -672,6 +684,8 @@ EKS_DEV unsigned k3_fwd_run(const SmoothArgs &a, const Plan3 &p, const Sched3 &s
           }
           j = look_back(fl, j, 1, -1, p.NCu, a.wait_ticks, ok);
         }
+        EKS_STAMP_AUX(0, 1, __builtin_amdgcn_s_memtime());
+        EKS_STAMP_AUX(0, 2, cu - 1 - j);
         if (lane_ok) {
           state_load_pl_wt<R>(fst, ((j + 1) * KPU) * KS, B, b, m, P);
           // fold the elements of units j+1 .. cu-1, the next one's loads in
@@ -1020,6 +1034,8 @@ EKS_DEV unsigned k3_bwd_run(const SmoothArgs &a, const Plan3 &p, const Sched3 &s
           }
           j = look_back(fl, j, 1, +1, p.NCc, a.wait_ticks, okc);
         }
+        EKS_STAMP_AUX(1, 1, __builtin_amdgcn_s_memtime());
+        EKS_STAMP_AUX(1, 2, j - cc - 1);
         if (lane_ok) {
 #pragma unroll
           for (int u = 0; u < R; ++u) ms[u] = ld_wt(&pl(inc, j * R + u, B, b));

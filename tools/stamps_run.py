@@ -51,3 +51,18 @@ for ps, kern in ((0, "k3_fwd"), (1, "k3_bwd")):
     print("  chain w0 percentiles 10/50/90/99:", np.percentile(ch, [10, 50, 90, 99]))
     fw = rows[:, 0, 2] - rows[:, 0, 1]
     print("  first phase w0 percentiles 10/50/90/99:", np.percentile(fw, [10, 50, 90, 99]))
+    # chain detail (EKS_STAMP_AUX): look-back end time in wave 1's slot 0,
+    # units folded in wave 2's; rows without a look-back keep (group, chunk)
+    tl, nf = rows[:, 1, 0], rows[:, 2, 0]
+    ok = (tl > rows[:, 0, 3]) & (tl <= rows[:, 0, 4])
+    if ok.any():
+        wait, fold = tl[ok] - rows[ok, 0, 3], rows[ok, 0, 4] - tl[ok]
+        print(f"  chain detail ({ok.sum()} of {len(rows)} units): wait mean {wait.mean():.0f} "
+              f"p50 {np.median(wait):.0f} p90 {np.percentile(wait, 90):.0f}; rest (fold, publish) "
+              f"mean {fold.mean():.0f} p50 {np.median(fold):.0f} p90 {np.percentile(fold, 90):.0f} cyc")
+        n = nf[ok]
+        for lo, hi in ((0, 0), (1, 3), (4, 7), (8, 15), (16, 63), (64, 1 << 30)):
+            sel = (n >= lo) & (n <= hi)
+            if sel.any():
+                print(f"    folded {lo:>3}-{hi if hi < 1 << 30 else 'inf':>3}: {sel.sum():6d} units, "
+                      f"wait {wait[sel].mean():7.0f}, rest {fold[sel].mean():7.0f} cyc")
