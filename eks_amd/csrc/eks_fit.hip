@@ -475,8 +475,20 @@ constexpr long long kLdsMaskT = kSelCompact ? 16384 : 65536;
 #define EKS_SEL_U 8
 #endif
 constexpr int kSelRowU = kSelCompact ? EKS_SEL_U : kSelU;
+// The register-row form (KPT > 0: rows <= 4 096 frames read once into 16 keys
+// per thread) is off by default since the compact layout: at T = 4 000 and
+// 17 408 rows the two-read form at 8 rows per CU selects in 0.30 ms, the
+// register form 0.33 ms at its own register budget (0.56 at 64 VGPRs, where
+// it spills), round 5's 0.40 (profiles/r06/ab_fit/ab_short_rows.txt).
+// EKS_SEL_REGROWS=1 builds it back for A/B runs.
+#ifndef EKS_SEL_KPT_WPE
+#define EKS_SEL_KPT_WPE 1
+#endif
+#ifndef EKS_SEL_REGROWS
+#define EKS_SEL_REGROWS 0
+#endif
 template <int BLK, int KPT = 0>
-__global__ __launch_bounds__(BLK, EKS_SEL_WPE) void k_fit_select(const double *__restrict__ worst,
+__global__ __launch_bounds__(BLK, KPT > 0 ? EKS_SEL_KPT_WPE : EKS_SEL_WPE) void k_fit_select(const double *__restrict__ worst,
                                                     long long TT, long long lo, long long hi,
                                                     double g, double *__restrict__ thr,
                                                     uint64_t *__restrict__ kept, long long W) {
@@ -2065,7 +2077,7 @@ extern "C" int eks_fit(const void *obs, int obs_dtype, int64_t B, int64_t T, int
     } else if (T >= 65536) {
       hipLaunchKernelGGL(k_fit_select<1024>, dim3((unsigned)B), dim3(1024), 0, s, worst, T,
                          lo, hi, g, thr, yev ? kept : nullptr, W);
-    } else if (T <= 256 * 16) {  // the row read once, into registers
+    } else if (EKS_SEL_REGROWS && T <= 256 * 16) {  // the row read once, into registers
       hipLaunchKernelGGL((k_fit_select<256, 16>), dim3((unsigned)B), dim3(256), 0, s, worst, T, lo,
                          hi, g, thr, yev ? kept : nullptr, W);
     } else {
