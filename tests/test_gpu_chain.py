@@ -167,3 +167,22 @@ def test_algo3_lookback_forms_bit_identical(torch, B, T):
         _lib.debug_set(_lib.EKS_DBG_A3_LB, prev)
     for k in ("out", "ms", "nll"):
         assert torch.equal(runs[2][k], runs[1][k]), k
+
+
+@pytest.mark.parametrize("algo,B,T", [(3, 2176, 2000), (2, 17, 100000)])
+def test_chained_passes_repeat_bit_identical(torch, algo, B, T):
+    """The in-launch hand-offs under repetition: 20 calls of the chained
+    passes on one input (algo 3 at the 8-GPU shard's 34 trajectory groups,
+    algo 2's chained group scans at config 2's geometry) all give the first
+    call's bits, and that result matches algo 1 (no hand-offs) to rounding.
+    tools/soak_handoff.py runs the same at 200 calls (profiles/r06/soak/)."""
+    from eks_amd import batch
+    d, params, flags = _singleview(torch, B, T, 31 + algo)
+    ref = batch.smooth(d, params, n=2, r=2, algo=1, flags=flags, want_nll=True)
+    first = batch.smooth(d, params, n=2, r=2, algo=algo, flags=flags, want_nll=True)
+    assert (first["status"] == 0).all()
+    assert float((first["out"] - ref["out"]).abs().max()) < 1e-8
+    for _ in range(20):
+        r = batch.smooth(d, params, n=2, r=2, algo=algo, flags=flags, want_nll=True)
+        assert torch.equal(r["out"], first["out"]) and torch.equal(r["nll"], first["nll"])
+        assert (r["status"] == 0).all()
