@@ -107,16 +107,15 @@ def test_mask_long_rows_whole_row_pass(torch):
     _vs_host(st, p, 25.0)
 
 
-@pytest.mark.parametrize("T,big,shift", [(16384, 2048, 50), (40000, 1536, 50),
+@pytest.mark.parametrize("T,big,shift", [(16384, 1536, 50), (40000, 1536, 50),
                                          (400000, 19968, 49)])
 def test_mask_bin_larger_than_lds(torch, T, big, shift):
     """No outliers and long rows: the threshold's top-digit bin holds more
-    frames than the LDS candidate buffer (2 048 32-bit keys for one block per
-    row of <= 16 384 frames with the hand-off planes, 1 536 64-bit keys for
-    the other one-block rows, both with 13-bit digits; 19 968 for the split
-    selection's final block with 14-bit digits) in at least one row, so the
-    select runs over the global row / candidate buffer and the mask comes
-    from the whole-row pass."""
+    frames than the LDS candidate buffer (1 536 keys for one block per row
+    with 13-bit digits -- at 16 384 frames the row still has its LDS mask, at
+    40 000 not; 19 968 for the split selection's final block with 14-bit
+    digits) in at least one row, so the select runs over the global row /
+    candidate buffer and the mask comes from the whole-row pass."""
     from eks_amd import synthetic
     from eks_amd.core import ensemble_array
     rng = np.random.default_rng(20000 + T)
