@@ -711,7 +711,7 @@ __global__ __launch_bounds__(BLK, KPT > 0 ? EKS_SEL_KPT_WPE : EKS_SEL_WPE) void 
 }
 
 // ---------------------------------------------------------------------------
-// The same selection for FEW long rows (B < kSelSplitB trajectories): one
+// The same selection for FEW long rows (sel_split_auto below): one
 // block per row leaves most of the chip idle (config 2: 17 blocks), so each
 // row is cut into segments of kSegKeys keys, one block per (row, segment),
 // in four launches:
@@ -729,7 +729,19 @@ __global__ __launch_bounds__(BLK, KPT > 0 ? EKS_SEL_KPT_WPE : EKS_SEL_WPE) void 
 //                numpy's _lerp, the bin's kept frames marked in the mask
 // Same threshold and mask bits as k_fit_select (tests/test_gpu_fit_mask.py).
 // ---------------------------------------------------------------------------
-constexpr long long kSelSplitB = 512;
+// The automatic choice (EKS_DBG_FIT_SELECT 0): the split for fewer than 64
+// rows, and for rows too long for the one-block kernel's LDS mask (the
+// whole-row marking pass, bins beyond its candidate buffer) up to 1 023 rows;
+// one block per row otherwise.  Whole device fits (tools/sel_split_timing.py,
+// profiles/r06/ab_fit/split_timing.txt), one block per row vs split:
+// T = 10 000, B = 64 / 512: 0.102 vs 0.118 / 0.188 vs 0.238 ms; T = 50 000,
+// B = 64 / 512: 0.256 vs 0.175 / 0.800 vs 0.672 ms.  (Round 5: split below
+// 512 rows whatever the length.)  Large B x T keeps one block per row: the
+// split's candidate buffers take B T 12 bytes.
+constexpr long long kSelSplitB = 64, kSelSplitLongB = 1024;
+bool sel_split_auto(long long B, long long T) {
+  return B < kSelSplitB || (T > kLdsMaskT && B < kSelSplitLongB);
+}
 // threads of the one-block-per-row selection for rows of 4 097 .. 65 535
 // frames (A/B builds: -DEKS_SEL_BLK=512)
 #ifndef EKS_SEL_BLK
@@ -1967,7 +1979,7 @@ extern "C" size_t eks_fit_workspace_bytes(int64_t B, int64_t T, int n) {
   // worst plane, thresholds, chunk partials, kept-frame mask, shifts K
   size_t bytes = (size_t)(B * T + B + B * (np + nc2) * len + B * W + B * n) * sizeof(double);
   // split selection: histograms, row states, candidate keys + indices
-  if (B < kSelSplitB || g_fit_select == 2)
+  if (sel_split_auto(B, T) || g_fit_select == 2)
     bytes += (size_t)B * kSplitBins * 4 + (size_t)B * sizeof(SelRow) + (size_t)B * T * 12 + 512;
   return bytes;
 }
@@ -2027,7 +2039,7 @@ extern "C" int eks_fit(const void *obs, int obs_dtype, int64_t B, int64_t T, int
       partB + B * (long long)((npart + kMergeFan - 1) / kMergeFan) * len);
   FitShift ks{reinterpret_cast<double *>(kept + B * W)};
   // split selection (few rows): its buffers after the shifts
-  const bool split_sel = g_fit_select == 1 ? false : g_fit_select == 2 ? true : B < kSelSplitB;
+  const bool split_sel = g_fit_select == 1 ? false : g_fit_select == 2 ? true : sel_split_auto(B, T);
   const int G = (int)((T + kSegKeys - 1) / kSegKeys);
   char *sel_base = reinterpret_cast<char *>(
       (reinterpret_cast<uintptr_t>(ks.K + B * n) + 255) / 256 * 256);  // 16-byte loads in k_sel_bin
